@@ -1,0 +1,251 @@
+/*
+ * lvg_amd.h — C ABI of the MI355X-native LVG level-population solver.
+ *
+ * This is the drop-in boundary for the reference's `calc_molecular_populations`
+ * layer loop (/root/reference/radiative_transfer/radiative_transfer.cpp:219-289)
+ * and the per-layer solve it drives:
+ *   iteration_control<iteration_scheme_lvg>::calculate_populations
+ *       (/root/reference/radiative_transfer/iteration_control.h:196-242)
+ *   iteration_scheme_lvg::calc_new_pop / operator() / intensity_calc
+ *       (/root/reference/radiative_transfer/iteration_lvg.cpp:87-185)
+ *   iteration_scheme_line_overlap::operator() / intensity_calc(u1,l1,u2,l2)
+ *       (/root/reference/radiative_transfer/iteration_lvg.cpp:348-501)
+ *   boundary_layer_populations (/root/reference/radiative_transfer/iteration_control.cpp:52-91)
+ *
+ * Plain C: no torch or HIP types cross this boundary. Every pointer in the
+ * description structs is a HOST pointer that is read during the call only
+ * (lvg_create copies all tables to the device; no pointer is retained).
+ * The only exception is lvg_solve_layers_device(), whose buffers are device
+ * pointers (inputs already resident in HBM).
+ *
+ * Units are the reference's CGS units: energies in cm^-1, masses in g,
+ * concentrations in cm^-3, velocities in cm/s, velocity gradients in s^-1,
+ * collision coefficients in cm^3 s^-1, dust cross sections in cm^2 per grain.
+ *
+ * Errors: every entry returns 0 on success and a negative LVG_E_* code
+ * otherwise; the text is available from lvg_last_error(). The library never
+ * exits. Non-convergence of a layer is NOT an error: it is reported per layer
+ * in lvg_layer_status (the reference's `bad_layers`, radiative_transfer.cpp:278-288).
+ *
+ * Threading: one handle per host thread; calls on a handle are synchronous.
+ */
+#ifndef LVG_AMD_H
+#define LVG_AMD_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LVG_ABI_VERSION 1
+
+/* ---- error codes ------------------------------------------------------- */
+#define LVG_OK            0
+#define LVG_E_ARG        -1   /* invalid argument / inconsistent description  */
+#define LVG_E_DEVICE     -2   /* HIP runtime error                             */
+#define LVG_E_NOMEM      -3   /* host or device allocation failed              */
+#define LVG_E_UNSUPPORTED -4  /* valid request this build does not implement   */
+#define LVG_E_STATE      -5   /* wrong call order / null handle                */
+
+/* ---- collision-partner species (concentration slots) ------------------- */
+/* The order of the arguments of collisional_transitions::set_gas_param
+ * (coll_rates.h:66-67): he, ph2, oh2, h, e. */
+enum lvg_species {
+    LVG_SP_HE  = 0,
+    LVG_SP_PH2 = 1,   /* for OH (non-HF) this slot carries n(H2, J=0) */
+    LVG_SP_OH2 = 2,   /* for OH (non-HF) this slot carries n(H2, J>=1) */
+    LVG_SP_H   = 3,
+    LVG_SP_E   = 4,
+    LVG_NB_SPECIES = 5
+};
+
+/* ---- molecule-specific collision rules ---------------------------------- */
+/* Each value selects the get_rate_neutrals/set_gas_param override of one
+ * reference collisional_transitions subclass. */
+enum lvg_coll_rule {
+    /* collisional_transitions base (coll_rates.cpp:181-197): every neutral table t
+     * with up < table.nb_lev contributes k_t * n[table.species]. */
+    LVG_COLL_GENERIC = 0,
+    /* ch3oh_collisions (coll_rates_ch3oh.cpp:472-533): tables {He, pH2, oH2}. */
+    LVG_COLL_CH3OH   = 1,
+    /* h2o_collisions (coll_rates_h2o.cpp:515-548): tables {He, He-rovib, pH2,
+     * oH2, H2-rovib, H} + electron tables. */
+    LVG_COLL_H2O     = 2,
+    /* oh_collisions (coll_rates_oh.cpp:323-347): tables {He, H2(J=0), H2(J>=1)}. */
+    LVG_COLL_OH      = 3,
+    /* oh_hf_collisions (coll_rates_oh.cpp:380-407): tables {He, pH2, oH2}. */
+    LVG_COLL_OH_HF   = 4
+};
+
+/* ---- initial-guess policy ---------------------------------------------- */
+enum lvg_init {
+    /* boundary_layer_populations for every layer: layers independent, sharded
+     * across CUs and GPUs (the reference's branch radiative_transfer.cpp:251-252). */
+    LVG_INIT_BOUNDARY_LAYER = 0,
+    /* pops_inout holds the initial guess of every layer. */
+    LVG_INIT_GIVEN          = 1,
+    /* the reference default (radiative_transfer.cpp:247-252): layer l starts from
+     * layer l-1's result when l-1 converged, else from boundary_layer_populations.
+     * Sequential across layers by construction. */
+    LVG_INIT_WARM_CHAIN     = 2
+};
+
+/* energy_level / energy_diagram / einstein_coeff (spectroscopy.h:46-87, :179-190) */
+typedef struct lvg_molecule {
+    int           nb_lev;   /* N                                                 */
+    double        mass;     /* molecule mass, g (molecule::mass)                */
+    const double *energy;   /* [N] level energies, cm^-1, strictly ascending     */
+    const int    *g;        /* [N] statistical weights                           */
+    const int    *v;        /* [N] vibrational/torsional number (CH3OH rule)     */
+    const double *j;        /* [N] angular momentum J (CH3OH rule)               */
+    const double *einst;    /* [N*N] einstein_coeff::arr row-major: einst[i*N+j] is
+                               the rate i->j; A_ul for i>j, g_u/g_l*A_ul for i<j */
+} lvg_molecule;
+
+/* collision_data (coll_rates.h:12-41): packed lower triangle, linear in T. */
+typedef struct lvg_coll_table {
+    int           nb_lev;   /* levels covered; imax = nb_lev*(nb_lev-1)/2        */
+    int           jmax;     /* number of temperature grid points                 */
+    const double *tgrid;    /* [jmax] K, ascending                               */
+    const double *coeff;    /* [imax*jmax] coeff[i*jmax+t], i = f*(f-1)/2 + s, f>s */
+    int           species;  /* LVG_COLL_GENERIC only: concentration slot (lvg_species) */
+} lvg_coll_table;
+
+typedef struct lvg_collisions {
+    int                   rule;        /* enum lvg_coll_rule                     */
+    int                   nb_neutral;  /* nb1 (coll_rates.h:59)                  */
+    int                   nb_electron; /* nb2 - nb1                              */
+    const lvg_coll_table *tables;      /* [nb_neutral + nb_electron], coll_data order */
+} lvg_collisions;
+
+/* dust_component::absorption (dust_model.cpp:473-490) */
+typedef struct lvg_dust_component {
+    int           nb_en;
+    double        wvl_exp;    /* long-wavelength exponent                         */
+    const double *energy;     /* [nb_en] cm^-1, ascending                         */
+    const double *abs_coeff;  /* [nb_en] absorption cross section per grain, cm^2 */
+} lvg_dust_component;
+
+typedef struct lvg_dust {
+    int                        nb_comp;
+    const lvg_dust_component  *comp;   /* [nb_comp] */
+} lvg_dust;
+
+/* lvg_method_data (lvg_method_functions.h:23-39): p(delta, gamma) */
+typedef struct lvg_esc_table {
+    int           nb_d, nb_g;
+    const double *delta;    /* [nb_d] ascending (raw, bilinear in raw values)     */
+    const double *gamma;    /* [nb_g] ascending                                   */
+    const double *p;        /* [nb_d*nb_g] p[k*nb_g + l]                          */
+} lvg_esc_table;
+
+/* lvg_line_overlap_data (lvg_method_functions.h:55-70) */
+typedef struct lvg_overlap_table {
+    int           nb_d, nb_dx, nb_gr, nb_g;
+    const double *log10_delta; /* [nb_d] log10(delta) grid (the file stores delta) */
+    const double *dx;          /* [nb_dx]                                          */
+    const double *gratio;      /* [nb_gr]                                          */
+    const double *gamma;       /* [nb_g]                                           */
+    const double *p;           /* [(nb_d*nb_dx)*(nb_gr*nb_g)]
+                                  p[(m*nb_dx+n)*(nb_gr*nb_g) + k*nb_g + l]         */
+} lvg_overlap_table;
+
+typedef struct lvg_problem {
+    const lvg_molecule      *mol;
+    const lvg_collisions    *coll;
+    const lvg_dust          *dust;
+    const lvg_esc_table     *esc;        /* lvg/lvg_loss_func.txt                 */
+    const lvg_overlap_table *overlap1;   /* line_overlap_func_p1 (NULL: no overlap) */
+    const lvg_overlap_table *overlap2;   /* line_overlap_func_p2                  */
+} lvg_problem;
+
+/* cloud_layer fields read by the solver (cloud_data.h:27-33), SoA [nb_lay]. */
+typedef struct lvg_layers {
+    int           nb_lay;
+    const double *temp_n, *temp_el;
+    const double *el_conc, *h_conc, *ph2_conc, *oh2_conc, *he_conc;
+    const double *mol_conc, *vel_turb, *vel_grad;
+    const double *dust_conc;   /* [nb_lay*nb_comp] grain concentrations          */
+} lvg_layers;
+
+/* Defaults (lvg_solve_opts_default): the reference's constants
+ * MAX_NB_ITER_ACC/EXT (radiative_transfer.cpp:26-27), rel_population_error
+ * (:45), accel start/period/nb (iteration_control.h:71). */
+typedef struct lvg_solve_opts {
+    double min_error;         /* 1e-5                                            */
+    int    max_iter_acc;      /* 150                                             */
+    int    max_iter_plain;    /* 15000                                           */
+    int    accel_start;       /* 40                                              */
+    int    accel_period;      /* 5                                               */
+    int    accel_nb;          /* 5 (nb_prev_steps)                               */
+    int    acceleration;      /* 1: Ng-type acceleration on                      */
+    int    allow_plain_retry; /* 1; 0 for CH3OHa/CH3OHe (radiative_transfer.cpp:259) */
+    int    init;              /* enum lvg_init                                   */
+    int    line_overlap;      /* 1: iteration_scheme_line_overlap (needs overlap tables) */
+} lvg_solve_opts;
+
+/* Per-layer outcome. */
+typedef struct lvg_layer_status {
+    int    converged;         /* is_found of the last calculate_populations call */
+    int    iterations;        /* calc_new_pop calls, all passes of this layer    */
+    int    used_plain_retry;  /* the non-accelerated retry pass ran              */
+    int    reserved;
+    double eq_error;          /* iteration_control::eq_error at exit             */
+    double rel_error;         /* iteration_control::rel_error at exit            */
+    double pop_error;         /* iteration_control::pop_error at exit            */
+} lvg_layer_status;
+
+typedef struct lvg_handle lvg_handle;
+
+/* ---- entry points -------------------------------------------------------- */
+int         lvg_abi_version(void);
+void        lvg_solve_opts_default(lvg_solve_opts *opts);
+
+/* Validate the description, build the packed device tables on `device`
+ * (HIP ordinal of this process). Replaces the object graph the reference
+ * builds before the layer loop: energy_diagram, einstein_coeff,
+ * collisional_transitions, dust_model, iteration_scheme_lvg(::init_molecule_data). */
+int         lvg_create(const lvg_problem *prob, int device, lvg_handle **out);
+void        lvg_destroy(lvg_handle *h);
+const char *lvg_last_error(const lvg_handle *h);   /* h may be NULL: last create error */
+int         lvg_nb_lev(const lvg_handle *h);
+
+/* Batched replacement of calc_molecular_populations' layer loop.
+ * pops_inout: host [nb_lay*N] layer-major (pop[l*N+i]); read when
+ * opts->init == LVG_INIT_GIVEN, always written. status: host [nb_lay] or NULL. */
+int         lvg_solve_layers(lvg_handle *h, const lvg_layers *layers, double *pops_inout,
+                             const lvg_solve_opts *opts, lvg_layer_status *status);
+
+/* Device-resident variant (all buffers already in HBM, stream = hipStream_t
+ * or NULL for the handle's stream). d_layer_soa is [10 + nb_comp][nb_lay] fp64
+ * in the field order of lvg_layers (temp_n, temp_el, el_conc, h_conc, ph2_conc,
+ * oh2_conc, he_conc, mol_conc, vel_turb, vel_grad, then dust_conc[c]) — see
+ * lvg_layer_soa_rows(). d_status: [nb_lay] lvg_layer_status. Asynchronous on
+ * `stream`; LVG_INIT_WARM_CHAIN is not accepted here. */
+int         lvg_layer_soa_rows(const lvg_handle *h);
+int         lvg_solve_layers_device(lvg_handle *h, int nb_lay, const double *d_layer_soa,
+                                    double *d_pops_inout, const lvg_solve_opts *opts,
+                                    lvg_layer_status *d_status, void *stream);
+
+/* One calc_new_pop (iteration_lvg.cpp:87-110) for layer `layer` on the device:
+ * returns the assembled rate matrix before LU (matrix_out [N*N] row-major,
+ * M[final][initial], row 0 = ones; may be NULL), the residual df (df_out [N],
+ * may be NULL), the new populations and eq_error. A debugging / parity probe. */
+int         lvg_debug_calc_new_pop(lvg_handle *h, const lvg_layers *layers, int layer,
+                                   const double *pop_in, int line_overlap,
+                                   double *matrix_out, double *df_out,
+                                   double *pop_out, double *eq_error);
+
+/* boundary_layer_populations (iteration_control.cpp:52-91) for every layer,
+ * on the device: pops_out host [nb_lay*N]. */
+int         lvg_boundary_layer_populations(lvg_handle *h, const lvg_layers *layers,
+                                           double *pops_out);
+
+/* Kernel timing of the last lvg_solve_layers* call on this handle, measured
+ * with HIP events on the stream the kernels ran on: total milliseconds of the
+ * solve kernel(s) and their count. */
+int         lvg_last_kernel_time(const lvg_handle *h, double *ms, int *nb_launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LVG_AMD_H */

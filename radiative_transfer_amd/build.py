@@ -1,0 +1,47 @@
+"""Build the HIP/C++ library (liblvg_amd.so) for gfx950, in-tree.
+
+hipcc cross-compiles without a GPU, so this runs in the CPU container as well
+as on the GPU box. The .so lands in radiative_transfer_amd/_lib/ and travels
+with the repository snapshot (git-ignored, not gpurun-ignored).
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB_DIR = os.path.join(PKG, "_lib")
+LIB = os.path.join(LIB_DIR, "liblvg_amd.so")
+SOURCES = ["lvg_kernels.hip", "lvg_abi.cpp"]
+HEADERS = ["lvg_device.h", os.path.join("..", "..", "include", "lvg_amd.h")]
+ARCH = os.environ.get("LVG_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB
+    os.makedirs(LIB_DIR, exist_ok=True)
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-function", "-o", LIB + ".tmp"]
+    cmd += [os.path.join(CSRC, f) for f in SOURCES]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

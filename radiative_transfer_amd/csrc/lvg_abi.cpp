@@ -1,0 +1,847 @@
+// lvg_abi.cpp — host side of the C ABI (include/lvg_amd.h): validation, the
+// packer that turns an lvg_problem into the device layout of lvg_device.h,
+// device memory, launches and HIP-event timing.
+//
+// The packer replaces the reference's object construction before the layer
+// loop (radiative_transfer.cpp:614-670 for CH3OH): the molecule rule of each
+// collisional_transitions subclass is compiled to per-pair term classes, the
+// line list of iteration_scheme_lvg::operator() (A > 0, iteration_lvg.cpp:134)
+// and the hfs_lines grouping of iteration_scheme_line_overlap::init_molecule_data
+// (iteration_lvg.cpp:317-346) are flattened, and the dust cross section at each
+// line energy (dust_model.cpp:473-490) is tabulated once.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/lvg_amd.h"
+#include "lvg_device.h"
+
+extern "C" hipError_t lvg_launch_solve(const LvgDevProblem *P, const LvgLaunch *L, int grid, hipStream_t s);
+extern "C" hipError_t lvg_launch_debug(const LvgDevProblem *P, const LvgLaunch *L, hipStream_t s);
+extern "C" int lvg_kernel_max_levels(void);
+extern "C" hipError_t lvg_kernel_occupancy(int *blocks_per_cu);
+
+namespace {
+
+thread_local std::string g_create_error;
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t n = 0;
+};
+
+struct ModeHost {
+    std::vector<int> u, l, unit0, unit1, dptr, dent;
+    std::vector<double> aul, alu, e, sigma;
+};
+
+}  // namespace
+
+struct lvg_handle {
+    int device = 0;
+    int N = 0;
+    int nb_comp = 0;
+    int has_overlap = 0;
+    int cus = 0, blocks_per_cu = 1;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    LvgDevProblem P{};
+    std::vector<DevBuf> bufs;
+    // workspace
+    double *ws = nullptr;
+    size_t ws_bytes = 0;
+    int64_t ws_stride = 0;
+    int *counter = nullptr;
+    // scratch for host-buffer solves
+    double *d_soa = nullptr, *d_pops = nullptr;
+    void *d_status = nullptr;
+    size_t soa_cap = 0, pops_cap = 0, status_cap = 0;
+    double last_ms = 0.;
+    int last_launches = 0;
+    // device-resident parameter blocks (kernels take pointers: no kernarg copies)
+    LvgDevProblem *d_prob = nullptr;
+    LvgLaunch *d_launch = nullptr;
+    int n_launch_slots = 0;
+    std::string err;
+};
+
+namespace {
+
+int fail(lvg_handle *h, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (h) h->err = buf; else g_create_error = buf;
+    return code;
+}
+
+#define HIPCHECK(h, x)                                                                   \
+    do {                                                                                 \
+        hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess) return fail(h, LVG_E_DEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+template <class T>
+int upload(lvg_handle *h, const T *src, size_t n, const T **dst) {
+    DevBuf b;
+    b.n = std::max<size_t>(1, n) * sizeof(T);
+    if (hipMalloc(&b.p, b.n) != hipSuccess) return fail(h, LVG_E_NOMEM, "hipMalloc(%zu) failed", b.n);
+    h->bufs.push_back(b);
+    if (n && hipMemcpy(b.p, src, n * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
+        return fail(h, LVG_E_DEVICE, "hipMemcpy H2D failed");
+    *dst = static_cast<const T *>(b.p);
+    return LVG_OK;
+}
+
+// dust_component::absorption (dust_model.cpp:473-490)
+double dust_sigma(const lvg_dust_component &c, double energy) {
+    const int n = c.nb_en;
+    if (energy < c.energy[0]) return c.abs_coeff[0] * std::pow(c.energy[0] / energy, c.wvl_exp);
+    if (energy > c.energy[n - 1]) return c.abs_coeff[n - 1];
+    int l = 0, r = n - 1;
+    while (r - l > 1) {
+        int i = l + ((r - l) >> 1);
+        if (c.energy[i] < energy) l = i; else r = i;
+    }
+    double deriv = (c.abs_coeff[l + 1] - c.abs_coeff[l]) / (c.energy[l + 1] - c.energy[l]);
+    return c.abs_coeff[l] + deriv * (energy - c.energy[l]);
+}
+
+// ---- rule compiler ----------------------------------------------------------
+struct TermList {
+    int nt = 0;
+    int table[LVG_MAX_TERMS];
+    int combo[LVG_MAX_TERMS];
+    int etable = -1;
+    bool operator<(const TermList &o) const {
+        if (nt != o.nt) return nt < o.nt;
+        for (int i = 0; i < nt; i++) {
+            if (table[i] != o.table[i]) return table[i] < o.table[i];
+            if (combo[i] != o.combo[i]) return combo[i] < o.combo[i];
+        }
+        return etable < o.etable;
+    }
+};
+
+struct Combos {
+    std::vector<std::vector<double>> w;
+    int get(std::vector<double> v) {
+        for (size_t i = 0; i < w.size(); i++) if (w[i] == v) return (int)i;
+        w.push_back(v);
+        return (int)w.size() - 1;
+    }
+};
+
+enum { HE = 0, PH2 = 1, OH2 = 2, HH = 3, EE = 4 };
+std::vector<double> sp(int s) { std::vector<double> v(5, 0.); v[s] = 1.; return v; }
+
+int compile_rule(lvg_handle *h, const lvg_problem *prob, std::vector<uint8_t> &pair_class, LvgTermTable &tt) {
+    const lvg_molecule &M = *prob->mol;
+    const lvg_collisions &C = *prob->coll;
+    const int N = M.nb_lev, nb1 = C.nb_neutral, nb2 = C.nb_neutral + C.nb_electron;
+    auto covers = [&](int t, int f) { return f < C.tables[t].nb_lev; };
+    Combos cb;
+    // fixed combo ids first so the common ones are stable
+    std::map<TermList, int> classes;
+    pair_class.assign((size_t)N * (N - 1) / 2, 0);
+    auto need = [&](int t, int f) -> bool {
+        if (t >= nb1) return false;
+        return covers(t, f);
+    };
+    for (int f = 1; f < N; f++) {
+        for (int s = 0; s < f; s++) {
+            TermList tl;
+            auto add = [&](int t, std::vector<double> w) {
+                tl.table[tl.nt] = t;
+                tl.combo[tl.nt] = cb.get(w);
+                tl.nt++;
+            };
+            switch (C.rule) {
+            case LVG_COLL_CH3OH: {                        // coll_rates_ch3oh.cpp:484-533
+                if (nb1 < 3) return fail(h, LVG_E_ARG, "CH3OH rule needs 3 neutral tables");
+                for (int t = 0; t < 3; t++)
+                    if (!covers(t, f)) return fail(h, LVG_E_ARG, "CH3OH table %d covers %d levels < %d", t, C.tables[t].nb_lev, N);
+                if (!M.v || !M.j) return fail(h, LVG_E_ARG, "CH3OH rule needs level v and J");
+                if (M.v[f] == M.v[s]) {
+                    if (M.v[f] == 0 && M.j[f] <= 9 && M.j[s] <= 9) { add(1, sp(PH2)); add(2, sp(OH2)); }
+                    else { std::vector<double> w(5, 0.); w[PH2] = 1.; w[OH2] = 1.; add(1, w); }
+                    add(0, sp(HE));
+                } else {
+                    std::vector<double> w(5, 0.); w[HE] = 1.; w[PH2] = 1.; w[OH2] = 3.;
+                    add(0, w);
+                }
+                break;
+            }
+            case LVG_COLL_H2O: {                          // coll_rates_h2o.cpp:530-548
+                if (nb1 < 6) return fail(h, LVG_E_ARG, "H2O rule needs 6 neutral tables");
+                if (f < 45) {
+                    const int ts[4] = {0, 2, 3, 5};
+                    const int ss[4] = {HE, PH2, OH2, HH};
+                    for (int q = 0; q < 4; q++) {
+                        if (!covers(ts[q], f)) return fail(h, LVG_E_ARG, "H2O table %d does not cover level %d", ts[q], f);
+                        add(ts[q], sp(ss[q]));
+                    }
+                } else {
+                    if (!covers(1, f) || !covers(4, f)) return fail(h, LVG_E_ARG, "H2O rovib tables do not cover level %d", f);
+                    std::vector<double> w1(5, 0.); w1[HE] = 1.; w1[HH] = 0.2;
+                    std::vector<double> w4(5, 0.); w4[PH2] = 1.; w4[OH2] = 1.;
+                    add(1, w1);
+                    add(4, w4);
+                }
+                break;
+            }
+            case LVG_COLL_OH:                             // coll_rates_oh.cpp:334-347
+            case LVG_COLL_OH_HF: {                        // coll_rates_oh.cpp:392-407
+                if (nb1 < 3) return fail(h, LVG_E_ARG, "OH rules need 3 neutral tables");
+                if (C.rule == LVG_COLL_OH && !covers(0, f))
+                    return fail(h, LVG_E_ARG, "OH He table must cover all levels (read unchecked, coll_rates_oh.cpp:336)");
+                if (covers(0, f)) add(0, sp(HE));
+                if (covers(1, f)) { add(1, sp(PH2)); add(2, sp(OH2)); }
+                break;
+            }
+            case LVG_COLL_GENERIC: {                      // coll_rates.cpp:181-197
+                for (int t = 0; t < nb1; t++) {
+                    if (tl.nt >= LVG_MAX_TERMS) return fail(h, LVG_E_UNSUPPORTED, "more than %d neutral tables", LVG_MAX_TERMS);
+                    int spc = C.tables[t].species;
+                    if (spc < 0 || spc >= LVG_NB_SPECIES) return fail(h, LVG_E_ARG, "table %d: bad species", t);
+                    if (need(t, f)) add(t, sp(spc));
+                }
+                break;
+            }
+            default:
+                return fail(h, LVG_E_ARG, "unknown collision rule %d", C.rule);
+            }
+            for (int t = nb1; t < nb2; t++)                // coll_rates.cpp:204-211
+                if (covers(t, f)) { tl.etable = t; break; }
+            auto it = classes.find(tl);
+            int id;
+            if (it == classes.end()) {
+                id = (int)classes.size();
+                if (id >= LVG_MAX_CLASSES) return fail(h, LVG_E_UNSUPPORTED, "too many collision term classes");
+                classes[tl] = id;
+            } else id = it->second;
+            pair_class[(size_t)f * (f - 1) / 2 + s] = (uint8_t)id;
+        }
+    }
+    if ((int)cb.w.size() > LVG_MAX_COMBOS) return fail(h, LVG_E_UNSUPPORTED, "too many concentration combinations");
+    memset(&tt, 0, sizeof tt);
+    for (int c = 0; c < LVG_MAX_CLASSES; c++) {
+        for (int k = 0; k < LVG_MAX_TERMS; k++) { tt.table[c][k] = -1; tt.combo[c][k] = 0; }
+        tt.etable[c] = -1;
+    }
+    for (auto &kv : classes) {
+        const TermList &tl = kv.first;
+        for (int k = 0; k < tl.nt; k++) { tt.table[kv.second][k] = (int8_t)tl.table[k]; tt.combo[kv.second][k] = (int8_t)tl.combo[k]; }
+        tt.etable[kv.second] = (int8_t)tl.etable;
+    }
+    tt.nb_combos = (int)cb.w.size();
+    for (size_t i = 0; i < cb.w.size(); i++)
+        for (int q = 0; q < 5; q++) tt.combo_w[i][q] = cb.w[i][q];
+    return LVG_OK;
+}
+
+// ---- line lists ------------------------------------------------------------------
+void add_line(ModeHost &m, const lvg_problem *prob, int u, int l) {
+    const lvg_molecule &M = *prob->mol;
+    const int N = M.nb_lev;
+    m.u.push_back(u);
+    m.l.push_back(l);
+    m.aul.push_back(M.einst[(size_t)u * N + l]);
+    m.alu.push_back(M.einst[(size_t)l * N + u]);
+    m.e.push_back(M.energy[u] - M.energy[l]);
+}
+
+void finish_mode(ModeHost &m, const lvg_problem *prob) {
+    const int N = prob->mol->nb_lev, nl = (int)m.u.size();
+    const int nc = prob->dust ? prob->dust->nb_comp : 0;
+    m.sigma.assign((size_t)std::max(1, nc) * std::max(1, nl), 0.);
+    for (int c = 0; c < nc; c++)
+        for (int n = 0; n < nl; n++) m.sigma[(size_t)c * nl + n] = dust_sigma(prob->dust->comp[c], m.e[n]);
+    std::vector<std::vector<int>> per(N);
+    for (int n = 0; n < nl; n++) {
+        per[m.u[n]].push_back(2 * n);
+        per[m.l[n]].push_back(2 * n + 1);
+    }
+    m.dptr.assign(N + 1, 0);
+    m.dent.clear();
+    for (int i = 0; i < N; i++) {
+        m.dptr[i] = (int)m.dent.size();
+        for (int e : per[i]) m.dent.push_back(e);
+    }
+    m.dptr[N] = (int)m.dent.size();
+}
+
+// hfs_lines::sort / split (iteration_lvg.cpp:259-302), stale minimum kept (quirk q6)
+struct Hfs {
+    int nb = 0, up[4], lo[4];
+    double en[4];
+    void swap_lines(int i, int j) { std::swap(up[i], up[j]); std::swap(lo[i], lo[j]); std::swap(en[i], en[j]); }
+    void sort() {
+        if (nb <= 2) return;
+        for (int i = 0; i < nb; i++)
+            for (int j = i + 1; j < nb; j++)
+                if (en[j] < en[i]) swap_lines(i, j);
+        int jj = 0;
+        double e = en[1] - en[0];
+        for (int i = 1; i < nb - 1; i++)
+            if (en[i + 1] - en[i] < e) jj = i;
+        e = en[jj];
+        for (int i = 0; i < nb; i++)
+            for (int j = i + 1; j < nb; j++)
+                if (std::fabs(en[j] - e) < std::fabs(en[i] - e)) swap_lines(i, j);
+    }
+};
+
+void build_overlap_mode(ModeHost &m, const lvg_problem *prob) {
+    const lvg_molecule &M = *prob->mol;
+    const int N = M.nb_lev;
+    auto group = [&](const Hfs &h, int start, int cnt) {
+        int n0 = (int)m.u.size();
+        add_line(m, prob, h.up[start], h.lo[start]);
+        int n1 = -1;
+        if (cnt == 2) { n1 = n0 + 1; add_line(m, prob, h.up[start + 1], h.lo[start + 1]); }
+        m.unit0.push_back(n0);
+        m.unit1.push_back(n1);
+    };
+    for (int i = 2; i < N; i += 2)
+        for (int j = 0; j < i; j += 2) {
+            Hfs h;
+            for (int a = 0; a < 2; a++)
+                for (int b = 0; b < 2; b++)
+                    if (M.einst[(size_t)(i + a) * N + j + b] > 1.e-99) {
+                        h.up[h.nb] = i + a; h.lo[h.nb] = j + b;
+                        h.en[h.nb] = M.energy[i + a] - M.energy[j + b];
+                        h.nb++;
+                    }
+            h.sort();
+            int start = 0;
+            if (h.nb >= 3) { group(h, 0, 2); start = 2; }
+            if (h.nb - start > 0) group(h, start, h.nb - start);
+        }
+    finish_mode(m, prob);
+}
+
+void build_plain_mode(ModeHost &m, const lvg_problem *prob) {
+    const lvg_molecule &M = *prob->mol;
+    const int N = M.nb_lev;
+    for (int i = 1; i < N; i++)
+        for (int j = 0; j < i; j++)
+            if (M.einst[(size_t)i * N + j] > 0.) {      // iteration_lvg.cpp:134
+                m.unit0.push_back((int)m.u.size());
+                m.unit1.push_back(-1);
+                add_line(m, prob, i, j);
+            }
+    finish_mode(m, prob);
+}
+
+int upload_mode(lvg_handle *h, const ModeHost &m, LvgModeLines &d) {
+    int rc;
+    d.nb_lines = (int)m.u.size();
+    d.nb_units = (int)m.unit0.size();
+    if ((rc = upload(h, m.u.data(), m.u.size(), &d.line_u))) return rc;
+    if ((rc = upload(h, m.l.data(), m.l.size(), &d.line_l))) return rc;
+    if ((rc = upload(h, m.aul.data(), m.aul.size(), &d.line_aul))) return rc;
+    if ((rc = upload(h, m.alu.data(), m.alu.size(), &d.line_alu))) return rc;
+    if ((rc = upload(h, m.e.data(), m.e.size(), &d.line_e))) return rc;
+    if ((rc = upload(h, m.sigma.data(), m.sigma.size(), &d.line_sigma))) return rc;
+    if ((rc = upload(h, m.unit0.data(), m.unit0.size(), &d.unit_l0))) return rc;
+    if ((rc = upload(h, m.unit1.data(), m.unit1.size(), &d.unit_l1))) return rc;
+    if ((rc = upload(h, m.dptr.data(), m.dptr.size(), &d.diag_ptr))) return rc;
+    if ((rc = upload(h, m.dent.data(), m.dent.size(), &d.diag_ent))) return rc;
+    return LVG_OK;
+}
+
+bool ascending(const double *a, int n, bool strict) {
+    for (int i = 1; i < n; i++)
+        if (strict ? !(a[i] > a[i - 1]) : !(a[i] >= a[i - 1])) return false;
+    return true;
+}
+
+int validate(lvg_handle *h, const lvg_problem *p) {
+    if (!p || !p->mol || !p->coll || !p->esc) return fail(h, LVG_E_ARG, "problem, molecule, collisions and escape table are required");
+    const lvg_molecule &M = *p->mol;
+    if (M.nb_lev < 2) return fail(h, LVG_E_ARG, "nb_lev must be >= 2");
+    if (M.nb_lev > lvg_kernel_max_levels())
+        return fail(h, LVG_E_UNSUPPORTED, "nb_lev %d exceeds this build's %d", M.nb_lev, lvg_kernel_max_levels());
+    if (!M.energy || !M.g || !M.einst || !(M.mass > 0.)) return fail(h, LVG_E_ARG, "molecule arrays / mass missing");
+    if (!ascending(M.energy, M.nb_lev, false)) return fail(h, LVG_E_ARG, "level energies must be ascending");
+    for (int i = 0; i < M.nb_lev; i++) if (M.g[i] <= 0) return fail(h, LVG_E_ARG, "g[%d] must be positive", i);
+    for (int i = 1; i < M.nb_lev; i++)
+        for (int j = 0; j < i; j++)
+            if (M.einst[(size_t)i * M.nb_lev + j] > 0. && !(M.energy[i] > M.energy[j]))
+                return fail(h, LVG_E_ARG, "line %d->%d has non-positive energy", i, j);
+    const lvg_collisions &C = *p->coll;
+    const int nt = C.nb_neutral + C.nb_electron;
+    if (C.nb_neutral < 0 || C.nb_electron < 0 || nt > LVG_MAX_TABLES || (nt && !C.tables))
+        return fail(h, LVG_E_ARG, "bad collision table counts");
+    for (int t = 0; t < nt; t++) {
+        const lvg_coll_table &T = C.tables[t];
+        if (T.jmax < 2 || T.nb_lev < 2 || !T.tgrid || !T.coeff) return fail(h, LVG_E_ARG, "collision table %d malformed", t);
+        if (!ascending(T.tgrid, T.jmax, true)) return fail(h, LVG_E_ARG, "collision table %d: tgrid not ascending", t);
+        if (T.nb_lev > M.nb_lev) {
+            // tables may cover more levels than the molecule uses; pairs beyond N are never read
+        }
+    }
+    const int nc = p->dust ? p->dust->nb_comp : 0;
+    if (nc > LVG_MAX_DUST) return fail(h, LVG_E_UNSUPPORTED, "more than %d dust components", LVG_MAX_DUST);
+    for (int c = 0; c < nc; c++) {
+        const lvg_dust_component &d = p->dust->comp[c];
+        if (d.nb_en < 2 || !ascending(d.energy, d.nb_en, true)) return fail(h, LVG_E_ARG, "dust component %d malformed", c);
+    }
+    if (p->esc->nb_d < 2 || p->esc->nb_g < 2 || !ascending(p->esc->delta, p->esc->nb_d, true) ||
+        !ascending(p->esc->gamma, p->esc->nb_g, true))
+        return fail(h, LVG_E_ARG, "escape table malformed");
+    if ((p->overlap1 == nullptr) != (p->overlap2 == nullptr)) return fail(h, LVG_E_ARG, "give both overlap tables or neither");
+    if (p->overlap1) {
+        const lvg_overlap_table *o[2] = {p->overlap1, p->overlap2};
+        for (auto t : o)
+            if (t->nb_d != o[0]->nb_d || t->nb_dx != o[0]->nb_dx || t->nb_gr != o[0]->nb_gr || t->nb_g != o[0]->nb_g ||
+                t->nb_d < 2 || t->nb_dx < 2 || t->nb_gr < 2 || t->nb_g < 2)
+                return fail(h, LVG_E_ARG, "overlap tables must share grids");
+        if (M.nb_lev % 2) return fail(h, LVG_E_ARG, "line overlap needs an even number of levels (hyperfine doublets)");
+    }
+    return LVG_OK;
+}
+
+int build(lvg_handle *h, const lvg_problem *p) {
+    const lvg_molecule &M = *p->mol;
+    const int N = M.nb_lev;
+    LvgDevProblem &D = h->P;
+    memset(&D, 0, sizeof D);
+    D.N = N;
+    D.mass = M.mass;
+    D.nb_comp = p->dust ? p->dust->nb_comp : 0;
+    D.nb_neutral = p->coll->nb_neutral;
+    D.nb_electron = p->coll->nb_electron;
+    D.nb_tables = D.nb_neutral + D.nb_electron;
+    int rc;
+    std::vector<double> g(N);
+    for (int i = 0; i < N; i++) g[i] = (double)M.g[i];
+    if ((rc = upload(h, M.energy, N, &D.energy))) return rc;
+    if ((rc = upload(h, g.data(), N, &D.g))) return rc;
+    if ((rc = upload(h, M.einst, (size_t)N * N, &D.einst))) return rc;
+    // collision tables, T-major, restricted to the levels the molecule uses
+    std::vector<int> jmax, nbl;
+    std::vector<int64_t> tgo, co;
+    std::vector<double> tg, cf;
+    for (int t = 0; t < D.nb_tables; t++) {
+        const lvg_coll_table &T = p->coll->tables[t];
+        const int nl = std::min(T.nb_lev, N);
+        const int64_t imax_src = (int64_t)T.nb_lev * (T.nb_lev - 1) / 2;
+        const int64_t imax = (int64_t)nl * (nl - 1) / 2;
+        (void)imax_src;
+        jmax.push_back(T.jmax);
+        nbl.push_back(nl);
+        tgo.push_back((int64_t)tg.size());
+        co.push_back((int64_t)cf.size());
+        tg.insert(tg.end(), T.tgrid, T.tgrid + T.jmax);
+        size_t base = cf.size();
+        cf.resize(base + (size_t)imax * T.jmax);
+        for (int64_t i = 0; i < imax; i++)
+            for (int j = 0; j < T.jmax; j++) cf[base + (size_t)j * imax + i] = T.coeff[(size_t)i * T.jmax + j];
+    }
+    if ((rc = upload(h, jmax.data(), jmax.size(), &D.tab_jmax))) return rc;
+    if ((rc = upload(h, nbl.data(), nbl.size(), &D.tab_nb_lev))) return rc;
+    if ((rc = upload(h, tgo.data(), tgo.size(), &D.tab_tg_off))) return rc;
+    if ((rc = upload(h, co.data(), co.size(), &D.tab_c_off))) return rc;
+    if ((rc = upload(h, tg.data(), tg.size(), &D.tab_tgrid))) return rc;
+    if ((rc = upload(h, cf.data(), cf.size(), &D.tab_coeff))) return rc;
+    std::vector<uint8_t> pc;
+    if ((rc = compile_rule(h, p, pc, D.terms))) return rc;
+    if ((rc = upload(h, pc.data(), pc.size(), &D.pair_class))) return rc;
+    // escape tables
+    D.esc_nd = p->esc->nb_d;
+    D.esc_ng = p->esc->nb_g;
+    if ((rc = upload(h, p->esc->delta, D.esc_nd, &D.esc_delta))) return rc;
+    if ((rc = upload(h, p->esc->gamma, D.esc_ng, &D.esc_gamma))) return rc;
+    if ((rc = upload(h, p->esc->p, (size_t)D.esc_nd * D.esc_ng, &D.esc_p))) return rc;
+    if (p->overlap1) {
+        const lvg_overlap_table &o = *p->overlap1;
+        D.ov_nd = o.nb_d; D.ov_ndx = o.nb_dx; D.ov_ngr = o.nb_gr; D.ov_ng = o.nb_g;
+        size_t n = (size_t)o.nb_d * o.nb_dx * o.nb_gr * o.nb_g;
+        if ((rc = upload(h, o.log10_delta, o.nb_d, &D.ov_ld))) return rc;
+        if ((rc = upload(h, o.dx, o.nb_dx, &D.ov_dx))) return rc;
+        if ((rc = upload(h, o.gratio, o.nb_gr, &D.ov_gr))) return rc;
+        if ((rc = upload(h, o.gamma, o.nb_g, &D.ov_g))) return rc;
+        if ((rc = upload(h, o.p, n, &D.ov_p1))) return rc;
+        if ((rc = upload(h, p->overlap2->p, n, &D.ov_p2))) return rc;
+        h->has_overlap = 1;
+        ModeHost mo;
+        build_overlap_mode(mo, p);
+        if ((rc = upload_mode(h, mo, D.overlap))) return rc;
+    }
+    ModeHost mp;
+    build_plain_mode(mp, p);
+    if ((rc = upload_mode(h, mp, D.plain))) return rc;
+    return LVG_OK;
+}
+
+int ensure_workspace(lvg_handle *h, int slots) {
+    const int N = h->N;
+    const int lines = std::max(h->P.plain.nb_lines, h->P.overlap.nb_lines);
+    int64_t stride = 2LL * N * N + 2LL * LVG_HIST_SLOTS * N + 3LL * N + 2LL * lines + 64;
+    stride = (stride + 31) & ~31LL;
+    size_t bytes = (size_t)stride * slots * sizeof(double);
+    if (bytes > h->ws_bytes) {
+        if (h->ws) (void)hipFree(h->ws);
+        h->ws = nullptr;
+        h->ws_bytes = 0;
+        if (hipMalloc(&h->ws, bytes) != hipSuccess) return fail(h, LVG_E_NOMEM, "workspace hipMalloc(%zu) failed", bytes);
+        h->ws_bytes = bytes;
+    }
+    h->ws_stride = stride;
+    return LVG_OK;
+}
+
+int check_opts(lvg_handle *h, const lvg_solve_opts *o) {
+    if (!o) return fail(h, LVG_E_ARG, "opts is NULL");
+    if (!(o->min_error > 0.) || o->max_iter_acc < 1 || o->max_iter_plain < 1)
+        return fail(h, LVG_E_ARG, "min_error / iteration caps invalid");
+    if (o->accel_nb < 2 || o->accel_nb > 5 || o->accel_period < 1 || (o->acceleration && o->accel_start < o->accel_nb))
+        return fail(h, LVG_E_ARG, "acceleration parameters invalid (accel_nb in [2,5], accel_start >= accel_nb)");
+    if (o->init < LVG_INIT_BOUNDARY_LAYER || o->init > LVG_INIT_WARM_CHAIN) return fail(h, LVG_E_ARG, "bad init mode");
+    if (o->line_overlap && !h->has_overlap) return fail(h, LVG_E_ARG, "line_overlap requested but no overlap tables");
+    return LVG_OK;
+}
+
+void fill_launch(lvg_handle *h, LvgLaunch &L, const lvg_solve_opts *o) {
+    memset(&L, 0, sizeof L);
+    L.min_error = o->min_error;
+    L.max_iter_acc = o->max_iter_acc;
+    L.max_iter_plain = o->max_iter_plain;
+    L.accel_start = o->accel_start;
+    L.accel_period = o->accel_period;
+    L.accel_nb = o->accel_nb;
+    L.acceleration = o->acceleration;
+    L.allow_plain_retry = o->allow_plain_retry;
+    L.init = o->init;
+    L.line_overlap = o->line_overlap;
+    L.ws = h->ws;
+    L.ws_stride = h->ws_stride;
+    L.counter = h->counter;
+}
+
+// copy launch parameter block `slot` to the device (stream-ordered)
+int push_launch(lvg_handle *h, const LvgLaunch &L, int slot, hipStream_t s, const LvgLaunch **dptr) {
+    if (slot >= h->n_launch_slots) {
+        int n = std::max(slot + 1, 2 * h->n_launch_slots);
+        LvgLaunch *p = nullptr;
+        if (h->d_launch) { (void)hipStreamSynchronize(s); (void)hipFree(h->d_launch); }
+        if (hipMalloc(&p, sizeof(LvgLaunch) * n) != hipSuccess) return fail(h, LVG_E_NOMEM, "launch block alloc failed");
+        h->d_launch = p;
+        h->n_launch_slots = n;
+    }
+    HIPCHECK(h, hipMemcpyAsync(h->d_launch + slot, &L, sizeof L, hipMemcpyHostToDevice, s));
+    *dptr = h->d_launch + slot;
+    return LVG_OK;
+}
+
+int grow(lvg_handle *h, void **p, size_t *cap, size_t bytes) {
+    if (bytes <= *cap) return LVG_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc(p, bytes) != hipSuccess) return fail(h, LVG_E_NOMEM, "hipMalloc(%zu) failed", bytes);
+    *cap = bytes;
+    return LVG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lvg_abi_version(void) { return LVG_ABI_VERSION; }
+
+void lvg_solve_opts_default(lvg_solve_opts *o) {
+    if (!o) return;
+    o->min_error = 1.e-5;       // rel_population_error, radiative_transfer.cpp:45
+    o->max_iter_acc = 150;      // MAX_NB_ITER_ACC, :27
+    o->max_iter_plain = 15000;  // MAX_NB_ITER_EXT, :26
+    o->accel_start = 40;        // iteration_control.h:71
+    o->accel_period = 5;
+    o->accel_nb = 5;
+    o->acceleration = 1;
+    o->allow_plain_retry = 1;
+    o->init = LVG_INIT_BOUNDARY_LAYER;
+    o->line_overlap = 0;
+}
+
+const char *lvg_last_error(const lvg_handle *h) { return h ? h->err.c_str() : g_create_error.c_str(); }
+
+int lvg_nb_lev(const lvg_handle *h) { return h ? h->N : 0; }
+
+int lvg_layer_soa_rows(const lvg_handle *h) { return h ? 10 + h->nb_comp : 0; }
+
+void lvg_destroy(lvg_handle *h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (auto &b : h->bufs) (void)hipFree(b.p);
+    if (h->ws) (void)hipFree(h->ws);
+    if (h->counter) (void)hipFree(h->counter);
+    if (h->d_soa) (void)hipFree(h->d_soa);
+    if (h->d_pops) (void)hipFree(h->d_pops);
+    if (h->d_status) (void)hipFree(h->d_status);
+    if (h->d_prob) (void)hipFree(h->d_prob);
+    if (h->d_launch) (void)hipFree(h->d_launch);
+    if (h->ev0) (void)hipEventDestroy(h->ev0);
+    if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+int lvg_create(const lvg_problem *prob, int device, lvg_handle **out) {
+    g_create_error.clear();
+    if (!out) return fail(nullptr, LVG_E_ARG, "out is NULL");
+    *out = nullptr;
+    lvg_handle *h = new (std::nothrow) lvg_handle();
+    if (!h) return fail(nullptr, LVG_E_NOMEM, "out of host memory");
+    int rc = validate(h, prob);
+    if (rc == LVG_OK) {
+        h->device = device;
+        hipError_t e = hipSetDevice(device);
+        if (e != hipSuccess) rc = fail(h, LVG_E_DEVICE, "hipSetDevice(%d): %s", device, hipGetErrorString(e));
+    }
+    if (rc == LVG_OK) {
+        h->N = prob->mol->nb_lev;
+        h->nb_comp = prob->dust ? prob->dust->nb_comp : 0;
+        rc = build(h, prob);
+    }
+    if (rc == LVG_OK) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) != hipSuccess ||
+            hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
+            hipMalloc(&h->counter, sizeof(int)) != hipSuccess)
+            rc = fail(h, LVG_E_DEVICE, "device setup failed");
+        else {
+            h->cus = prop.multiProcessorCount;
+            if (hipMalloc(&h->d_prob, sizeof(LvgDevProblem)) != hipSuccess ||
+                hipMemcpy(h->d_prob, &h->P, sizeof(LvgDevProblem), hipMemcpyHostToDevice) != hipSuccess)
+                rc = fail(h, LVG_E_DEVICE, "problem block upload failed");
+            int b = 1;
+            if (lvg_kernel_occupancy(&b) != hipSuccess || b < 1) b = 1;
+            h->blocks_per_cu = b;
+        }
+    }
+    if (rc != LVG_OK) {
+        g_create_error = h->err;
+        lvg_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return LVG_OK;
+}
+
+int lvg_solve_layers_device(lvg_handle *h, int nb_lay, const double *d_soa, double *d_pops,
+                            const lvg_solve_opts *o, lvg_layer_status *d_status, void *stream) {
+    if (!h) return LVG_E_STATE;
+    int rc = check_opts(h, o);
+    if (rc) return rc;
+    if (o->init == LVG_INIT_WARM_CHAIN) return fail(h, LVG_E_ARG, "warm chain is only available through lvg_solve_layers");
+    if (nb_lay < 0 || (nb_lay > 0 && (!d_soa || !d_pops || !d_status))) return fail(h, LVG_E_ARG, "bad device buffers");
+    h->last_ms = 0.;
+    h->last_launches = 0;
+    if (nb_lay == 0) return LVG_OK;
+    HIPCHECK(h, hipSetDevice(h->device));
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    const int grid = std::max(1, std::min(nb_lay, h->cus * h->blocks_per_cu));
+    if ((rc = ensure_workspace(h, grid))) return rc;
+    LvgLaunch L;
+    fill_launch(h, L, o);
+    L.nb_lay = nb_lay;
+    L.lay_offset = 0;
+    L.soa_ld = nb_lay;
+    L.soa = d_soa;
+    L.pops = d_pops;
+    L.status = d_status;
+    const LvgLaunch *dL = nullptr;
+    if ((rc = push_launch(h, L, 0, s, &dL))) return rc;
+    HIPCHECK(h, hipMemsetAsync(h->counter, 0, sizeof(int), s));
+    HIPCHECK(h, hipEventRecord(h->ev0, s));
+    HIPCHECK(h, lvg_launch_solve(h->d_prob, dL, grid, s));
+    HIPCHECK(h, hipEventRecord(h->ev1, s));
+    h->last_launches = 1;
+    if (!stream) {
+        HIPCHECK(h, hipStreamSynchronize(s));
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, h->ev0, h->ev1);
+        h->last_ms = ms;
+    }
+    return LVG_OK;
+}
+
+int lvg_last_kernel_time(const lvg_handle *h, double *ms, int *nb) {
+    if (!h) return LVG_E_STATE;
+    lvg_handle *hh = const_cast<lvg_handle *>(h);
+    if (hh->last_launches && hh->last_ms == 0.) {
+        float f = 0.f;
+        if (hipEventSynchronize(hh->ev1) == hipSuccess && hipEventElapsedTime(&f, hh->ev0, hh->ev1) == hipSuccess)
+            hh->last_ms = f;
+    }
+    if (ms) *ms = hh->last_ms;
+    if (nb) *nb = hh->last_launches;
+    return LVG_OK;
+}
+
+static int upload_layers(lvg_handle *h, const lvg_layers *L) {
+    const int nl = L->nb_lay, rows = 10 + h->nb_comp;
+    std::vector<double> soa((size_t)rows * nl);
+    const double *f[10] = {L->temp_n, L->temp_el, L->el_conc, L->h_conc, L->ph2_conc,
+                           L->oh2_conc, L->he_conc, L->mol_conc, L->vel_turb, L->vel_grad};
+    for (int r = 0; r < 10; r++) {
+        if (!f[r]) return fail(h, LVG_E_ARG, "layer field %d is NULL", r);
+        memcpy(&soa[(size_t)r * nl], f[r], sizeof(double) * nl);
+    }
+    if (h->nb_comp && !L->dust_conc) return fail(h, LVG_E_ARG, "dust_conc is NULL");
+    for (int c = 0; c < h->nb_comp; c++)
+        for (int l = 0; l < nl; l++) soa[(size_t)(10 + c) * nl + l] = L->dust_conc[(size_t)l * h->nb_comp + c];
+    int rc = grow(h, (void **)&h->d_soa, &h->soa_cap, soa.size() * sizeof(double));
+    if (rc) return rc;
+    HIPCHECK(h, hipMemcpyAsync(h->d_soa, soa.data(), soa.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    HIPCHECK(h, hipStreamSynchronize(h->stream));
+    return LVG_OK;
+}
+
+int lvg_solve_layers(lvg_handle *h, const lvg_layers *layers, double *pops, const lvg_solve_opts *o,
+                     lvg_layer_status *status) {
+    if (!h) return LVG_E_STATE;
+    if (!layers || (layers->nb_lay > 0 && !pops)) return fail(h, LVG_E_ARG, "layers / pops missing");
+    int rc = check_opts(h, o);
+    if (rc) return rc;
+    const int nl = layers->nb_lay, N = h->N;
+    if (nl == 0) return LVG_OK;
+    HIPCHECK(h, hipSetDevice(h->device));
+    if ((rc = upload_layers(h, layers))) return rc;
+    if ((rc = grow(h, (void **)&h->d_pops, &h->pops_cap, sizeof(double) * (size_t)nl * N))) return rc;
+    if ((rc = grow(h, &h->d_status, &h->status_cap, sizeof(lvg_layer_status) * (size_t)nl))) return rc;
+    if (o->init != LVG_INIT_BOUNDARY_LAYER)
+        HIPCHECK(h, hipMemcpyAsync(h->d_pops, pops, sizeof(double) * (size_t)nl * N, hipMemcpyHostToDevice, h->stream));
+    if (o->init == LVG_INIT_WARM_CHAIN) {
+        // the reference default: sequential chain, one layer per launch
+        if ((rc = ensure_workspace(h, 1))) return rc;
+        LvgLaunch L;
+        fill_launch(h, L, o);
+        L.soa = h->d_soa;
+        L.soa_ld = nl;
+        L.nb_lay = 1;
+        L.chain = 1;
+        std::vector<const LvgLaunch *> dls(nl);
+        for (int l = 0; l < nl; l++) {
+            L.lay_offset = l;
+            L.pops = h->d_pops + (size_t)l * N;
+            L.status = (lvg_layer_status *)h->d_status + l;
+            if ((rc = push_launch(h, L, l, h->stream, &dls[l]))) return rc;
+        }
+        for (int l = 0; l < nl; l++) dls[l] = h->d_launch + l;   // the block may have been reallocated
+        for (int l = 0; l < nl; l++) {
+            L.lay_offset = l;
+            L.pops = h->d_pops + (size_t)l * N;
+            L.status = (lvg_layer_status *)h->d_status + l;
+            HIPCHECK(h, hipMemcpyAsync(h->d_launch + l, &L, sizeof L, hipMemcpyHostToDevice, h->stream));
+        }
+        HIPCHECK(h, hipStreamSynchronize(h->stream));
+        HIPCHECK(h, hipEventRecord(h->ev0, h->stream));
+        for (int l = 0; l < nl; l++) {
+            HIPCHECK(h, hipMemsetAsync(h->counter, 0, sizeof(int), h->stream));
+            HIPCHECK(h, lvg_launch_solve(h->d_prob, dls[l], 1, h->stream));
+        }
+        HIPCHECK(h, hipEventRecord(h->ev1, h->stream));
+        HIPCHECK(h, hipStreamSynchronize(h->stream));
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, h->ev0, h->ev1);
+        h->last_ms = ms;
+        h->last_launches = nl;
+    } else {
+        rc = lvg_solve_layers_device(h, nl, h->d_soa, h->d_pops, o, (lvg_layer_status *)h->d_status, nullptr);
+        if (rc) return rc;
+    }
+    HIPCHECK(h, hipMemcpy(pops, h->d_pops, sizeof(double) * (size_t)nl * N, hipMemcpyDeviceToHost));
+    if (status) HIPCHECK(h, hipMemcpy(status, h->d_status, sizeof(lvg_layer_status) * (size_t)nl, hipMemcpyDeviceToHost));
+    return LVG_OK;
+}
+
+int lvg_debug_calc_new_pop(lvg_handle *h, const lvg_layers *layers, int layer, const double *pop_in, int line_overlap,
+                           double *matrix_out, double *df_out, double *pop_out, double *eq_error) {
+    if (!h) return LVG_E_STATE;
+    if (!layers || layer < 0 || layer >= layers->nb_lay || !pop_in || !pop_out)
+        return fail(h, LVG_E_ARG, "bad debug arguments");
+    if (line_overlap && !h->has_overlap) return fail(h, LVG_E_ARG, "no overlap tables");
+    const int N = h->N;
+    HIPCHECK(h, hipSetDevice(h->device));
+    int rc = upload_layers(h, layers);
+    if (rc) return rc;
+    if ((rc = ensure_workspace(h, 1))) return rc;
+    double *dbg = nullptr;
+    HIPCHECK(h, hipMalloc(&dbg, sizeof(double) * ((size_t)N * N + 3 * N + 1)));
+    lvg_solve_opts o;
+    lvg_solve_opts_default(&o);
+    o.line_overlap = line_overlap;
+    LvgLaunch L;
+    fill_launch(h, L, &o);
+    L.soa = h->d_soa;
+    L.soa_ld = layers->nb_lay;
+    L.lay_offset = layer;
+    L.nb_lay = 1;
+    L.dbg_matrix = dbg;
+    L.dbg_df = dbg + (size_t)N * N;            // N + 1 (eq_error at [N])
+    L.dbg_pop_in = L.dbg_df + N + 1;
+    L.pops = L.dbg_pop_in + N;
+    const LvgLaunch *dL = nullptr;
+    if ((rc = push_launch(h, L, 0, h->stream, &dL))) { (void)hipFree(dbg); return rc; }
+    hipError_t e = hipMemcpy(L.dbg_pop_in, pop_in, sizeof(double) * N, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e == hipSuccess) e = lvg_launch_debug(h->d_prob, dL, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    std::vector<double> host((size_t)N * N + 3 * N + 1);
+    if (e == hipSuccess) e = hipMemcpy(host.data(), dbg, sizeof(double) * host.size(), hipMemcpyDeviceToHost);
+    (void)hipFree(dbg);
+    if (e != hipSuccess) return fail(h, LVG_E_DEVICE, "debug kernel: %s", hipGetErrorString(e));
+    if (matrix_out) memcpy(matrix_out, host.data(), sizeof(double) * N * N);
+    if (df_out) memcpy(df_out, host.data() + (size_t)N * N, sizeof(double) * N);
+    if (eq_error) *eq_error = host[(size_t)N * N + N];
+    memcpy(pop_out, host.data() + (size_t)N * N + 2 * N + 1, sizeof(double) * N);
+    return LVG_OK;
+}
+
+int lvg_boundary_layer_populations(lvg_handle *h, const lvg_layers *layers, double *pops_out) {
+    if (!h) return LVG_E_STATE;
+    if (!layers || !pops_out) return fail(h, LVG_E_ARG, "bad arguments");
+    const int nl = layers->nb_lay, N = h->N;
+    if (nl == 0) return LVG_OK;
+    HIPCHECK(h, hipSetDevice(h->device));
+    int rc = upload_layers(h, layers);
+    if (rc) return rc;
+    if ((rc = grow(h, (void **)&h->d_pops, &h->pops_cap, sizeof(double) * (size_t)nl * N))) return rc;
+    if ((rc = grow(h, &h->d_status, &h->status_cap, sizeof(lvg_layer_status) * (size_t)nl))) return rc;
+    const int grid = std::max(1, std::min(nl, h->cus * h->blocks_per_cu));
+    if ((rc = ensure_workspace(h, grid))) return rc;
+    lvg_solve_opts o;
+    lvg_solve_opts_default(&o);
+    LvgLaunch L;
+    fill_launch(h, L, &o);
+    L.soa = h->d_soa;
+    L.soa_ld = nl;
+    L.nb_lay = nl;
+    L.pops = h->d_pops;
+    L.status = h->d_status;
+    L.dbg_mode = 2;
+    const LvgLaunch *dL = nullptr;
+    if ((rc = push_launch(h, L, 0, h->stream, &dL))) return rc;
+    HIPCHECK(h, hipMemsetAsync(h->counter, 0, sizeof(int), h->stream));
+    HIPCHECK(h, lvg_launch_solve(h->d_prob, dL, grid, h->stream));
+    HIPCHECK(h, hipStreamSynchronize(h->stream));
+    HIPCHECK(h, hipMemcpy(pops_out, h->d_pops, sizeof(double) * (size_t)nl * N, hipMemcpyDeviceToHost));
+    return LVG_OK;
+}
+
+}  // extern "C"

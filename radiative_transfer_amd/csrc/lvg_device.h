@@ -1,0 +1,81 @@
+// lvg_device.h — packed, device-resident form of an lvg_problem (built once in
+// lvg_create) and the per-launch parameter block of the solve kernels.
+//
+// Layout choices (HBM, all fp64 unless noted):
+//  * collision tables are stored T-major, coeff[t][pair] (pair = f(f-1)/2 + s), so a
+//    wavefront that walks consecutive level pairs at one temperature index reads
+//    contiguous bytes (coll_rates.cpp:54-59 reads coeff[pair][t]);
+//  * the molecule rule (coll_rates_{ch3oh,h2o,oh}.cpp get_rate_neutrals) is compiled
+//    on the host into a per-pair class byte plus a small class table of
+//    (table, concentration-combination) terms, so the device evaluates
+//    sum_k k_table(T) * n_combo with no molecule branches;
+//  * radiative lines are a flat list (u, l, A_ul, A_lu, E, sigma_dust[c]) plus
+//    "units" (1 line, or 2 overlapping lines of iteration_scheme_line_overlap) and a
+//    per-level CSR of (line, role) used to form the diagonal deterministically.
+#pragma once
+#include <stdint.h>
+
+#define LVG_MAX_TABLES   16
+#define LVG_MAX_TERMS    6
+#define LVG_MAX_CLASSES  32
+#define LVG_MAX_COMBOS   16
+#define LVG_MAX_DUST     4
+#define LVG_HIST_SLOTS   8      // ring slots for prev_level_pop / residual_list
+
+struct LvgTermTable {
+    int8_t table[LVG_MAX_CLASSES][LVG_MAX_TERMS];  // neutral terms, -1 = none
+    int8_t combo[LVG_MAX_CLASSES][LVG_MAX_TERMS];
+    int8_t etable[LVG_MAX_CLASSES];                // first applicable electron table, -1 = none
+    double combo_w[LVG_MAX_COMBOS][5];             // combo = sum_s w[s] * n[s] (he, ph2, oh2, h, e)
+    int    nb_combos;
+};
+
+struct LvgModeLines {          // one radiative scheme (plain LVG or line overlap)
+    int nb_lines, nb_units;
+    const int    *line_u, *line_l;
+    const double *line_aul, *line_alu, *line_e;
+    const double *line_sigma;  // [nb_comp][nb_lines] dust cross section at the line energy
+    const int    *unit_l0, *unit_l1;   // unit -> line index (l1 = -1 for a single line)
+    const int    *diag_ptr;    // [N+1]
+    const int    *diag_ent;    // line*2 + role (0: level is upper -> y1, 1: lower -> y2)
+};
+
+struct LvgDevProblem {
+    int N, nb_comp, nb_tables, nb_neutral, nb_electron;
+    double mass;
+    const double *energy;      // [N]
+    const double *g;           // [N]
+    const double *einst;       // [N*N]
+    // collision tables
+    const int     *tab_jmax, *tab_nb_lev;
+    const int64_t *tab_tg_off, *tab_c_off;
+    const double  *tab_tgrid, *tab_coeff;          // T-major coeff[t][pair]
+    const uint8_t *pair_class;                     // [N(N-1)/2]
+    LvgTermTable   terms;
+    // LVG escape table (lvg_method_functions.cpp:74-110)
+    int esc_nd, esc_ng;
+    const double *esc_delta, *esc_gamma, *esc_p;
+    // line-overlap tables (lvg_method_functions.cpp:324-392)
+    int ov_nd, ov_ndx, ov_ngr, ov_ng;
+    const double *ov_ld, *ov_dx, *ov_gr, *ov_g, *ov_p1, *ov_p2;
+    LvgModeLines plain, overlap;
+};
+
+// Per-launch options / buffers.
+struct LvgLaunch {
+    int nb_lay, lay_offset, soa_ld;   // layer SoA row stride (= total layers of the SoA)
+    const double *soa;                // [10 + nb_comp][soa_ld]
+    double       *pops;               // [nb_lay][N] (layer index relative to lay_offset)
+    void         *status;             // lvg_layer_status[nb_lay]
+    double        min_error;
+    int max_iter_acc, max_iter_plain, accel_start, accel_period, accel_nb;
+    int acceleration, allow_plain_retry, init, line_overlap;
+    int chain;                        // warm-chain launch: layer lay_offset uses pops/status of lay_offset-1
+    // workspace (per resident block slot)
+    double   *ws;                     // [nb_slots][ws_stride]
+    int64_t   ws_stride;
+    int      *counter;                // work queue head
+    // debug probe outputs (lvg_debug_calc_new_pop)
+    double   *dbg_matrix, *dbg_df, *dbg_pop_in;
+    int       dbg_mode;               // 0 solve, 1 debug calc_new_pop, 2 boundary pops only
+};

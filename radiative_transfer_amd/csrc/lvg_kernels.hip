@@ -1,0 +1,865 @@
+// lvg_kernels.hip — MI355X (gfx950) kernels of the LVG level-population solver.
+//
+// One 256-thread workgroup owns one cloud layer at a time and runs the whole
+// reference per-layer pipeline on the device (radiative_transfer.cpp:236-288):
+// layer parameters (iteration_lvg.cpp:59-85), collision operator
+// (coll_rates*.cpp get_rate_*), boundary_layer_populations (iteration_control.cpp:52-91),
+// the iteration_control fixed-point loop with Ng acceleration
+// (iteration_control.h:84-242), and per iteration the rate-matrix assembly,
+// residual and LU solve of calc_new_pop (iteration_lvg.cpp:87-161).
+//
+// The grid is persistent: blocks pull layers from an atomic work queue, so
+// layers with very different iteration counts balance across CUs, and each
+// block's scratch (collision operator K, working matrix A, Ng history) lives in
+// a per-slot HBM workspace that stays L2/MALL resident while the slot works.
+//
+// fp64 throughout, no MFMA: the dense work is a batched small LU (blocked,
+// right-looking, NB-wide panels in LDS, 4x4 register-tiled trailing update).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "lvg_device.h"
+#include "../../include/lvg_amd.h"
+
+namespace lvg {
+
+constexpr int BT   = 256;   // threads per workgroup
+constexpr int NW   = BT / 64;
+constexpr int NB   = 16;    // LU panel width
+constexpr int NMAX = 256;   // max levels of this kernel
+constexpr int NHIST = LVG_HIST_SLOTS;
+
+constexpr double BOLTZMANN_CONSTANT    = 1.380649e-16;
+constexpr double CM_INVERSE_TO_KELVINS = 1.438776877;
+constexpr double EIGHT_PI              = 25.132741228718345;
+constexpr double SPEED_OF_LIGHT        = 2.99792458e+10;
+constexpr double MIN_COLLISION_RATE    = 1.e-99;
+constexpr double INV_TRANS_FACTOR      = -0.1;
+constexpr double MIN_LINE_OPACITY      = 1.e-99;
+
+struct Smem {
+    double pold[NMAX], pnew[NMAX], bvec[NMAX];
+    double red[64];
+    int    ired[64];
+    int    piv[NB];
+    double L11[NB][NB + 1];
+    double LT[NB][NMAX + 4];
+    union {
+        double P[NMAX][NB + 1];
+        double U[NB][NMAX + 4];
+    } pu;
+    // per-layer scalars
+    double T, Te, vw, vgrad, nmol, ne;
+    double cc[LVG_MAX_COMBOS];
+    double teff[LVG_MAX_TABLES];
+    int    lo[LVG_MAX_TABLES];
+    double dust[LVG_MAX_DUST];
+    double hist_acc[32];
+    int    layer;
+};
+
+// ------------------------------------------------------------------------------
+// small helpers
+// ------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+
+// block max of a non-negative quantity (NaN-propagating like the reference's
+// "if (e < x) e = x" scan is not needed: inputs are finite in practice)
+__device__ __forceinline__ double block_max(double v, Smem &sm) {
+    const int t = threadIdx.x, w = t >> 6;
+    v = wave_max(v);
+    __syncthreads();
+    if ((t & 63) == 0) sm.red[w] = v;
+    __syncthreads();
+    double r = sm.red[0];
+#pragma unroll
+    for (int i = 1; i < NW; i++) r = fmax(r, sm.red[i]);
+    return r;
+}
+
+// argmax with ties to the smallest index (the oracle's first-maximum rule)
+__device__ __forceinline__ int block_argmax(double v, int idx, Smem &sm) {
+    const int t = threadIdx.x, w = t >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        double ov = __shfl_xor(v, o);
+        int oi = __shfl_xor(idx, o);
+        if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
+    }
+    if ((t & 63) == 0) { sm.red[w] = v; sm.ired[w] = idx; }
+    __syncthreads();
+    double bv = sm.red[0];
+    int bi = sm.ired[0];
+#pragma unroll
+    for (int i = 1; i < NW; i++) {
+        double ov = sm.red[i];
+        int oi = sm.ired[i];
+        if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    return bi;
+}
+
+// locate_index restatement: -1 below, n-1 above, else a[j] <= x < a[j+1]
+__device__ __forceinline__ int locate_index(const double *a, int n, double x) {
+    if (x < a[0]) return -1;
+    if (x > a[n - 1]) return n - 1;
+    int l = 0, r = n - 1;
+    while (r - l > 1) {
+        int m = l + ((r - l) >> 1);
+        if (a[m] <= x) l = m; else r = m;
+    }
+    return l;
+}
+
+// lvg_method_data::get_esc_func (lvg_method_functions.cpp:74-110)
+__device__ __forceinline__ double esc_func(const LvgDevProblem &P, double gamma, double delta) {
+    const int nd = P.esc_nd, ng = P.esc_ng;
+    int k = locate_index(P.esc_delta, nd, delta);
+    int l = locate_index(P.esc_gamma, ng, gamma);
+    double t, u;
+    if (k < 0) { t = 0.; k = 0; }
+    else if (k > nd - 2) { t = 1.; k = nd - 2; }
+    else t = (delta - P.esc_delta[k]) / (P.esc_delta[k + 1] - P.esc_delta[k]);
+    if (l < 0) { l = 0; u = 0.; }
+    else if (l > ng - 2) { l = ng - 2; u = 1.; }
+    else u = (gamma - P.esc_gamma[l]) / (P.esc_gamma[l + 1] - P.esc_gamma[l]);
+    const double *p = P.esc_p;
+    double e = p[k * ng + l] * (1. - t) * (1. - u) + p[(k + 1) * ng + l] * t * (1. - u)
+             + p[k * ng + l + 1] * (1. - t) * u + p[(k + 1) * ng + l + 1] * u * t;
+    return e > 1. ? 1. : (e < 0. ? 0. : e);
+}
+
+// lvg_line_overlap_data::get_esc_func (lvg_method_functions.cpp:324-392)
+__device__ __forceinline__ double overlap_esc_func(const LvgDevProblem &P, const double *tab, double gamma, double delta,
+                                   double gratio, double dxv) {
+    delta = log10(delta);
+    int m = locate_index(P.ov_ld, P.ov_nd, delta);
+    int l = locate_index(P.ov_g, P.ov_ng, gamma);
+    int k = locate_index(P.ov_gr, P.ov_ngr, gratio);
+    int n = locate_index(P.ov_dx, P.ov_ndx, dxv);
+    double y = 0., u = 0., t = 0., p = 0.;
+    if (m < 0) m = 0;
+    else if (m > P.ov_nd - 2) { m = P.ov_nd - 2; y = 1.; }
+    else y = (delta - P.ov_ld[m]) / (P.ov_ld[m + 1] - P.ov_ld[m]);
+    if (n < 0) n = 0;
+    else if (n > P.ov_ndx - 2) { p = 1.; n = P.ov_ndx - 2; }
+    else p = (dxv - P.ov_dx[n]) / (P.ov_dx[n + 1] - P.ov_dx[n]);
+    if (l < 0) l = 0;
+    else if (l > P.ov_ng - 2) { l = P.ov_ng - 2; u = 1.; }
+    else u = (gamma - P.ov_g[l]) / (P.ov_g[l + 1] - P.ov_g[l]);
+    if (k < 0) k = 0;
+    else if (k > P.ov_ngr - 2) { t = 1.; k = P.ov_ngr - 2; }
+    else t = (gratio - P.ov_gr[k]) / (P.ov_gr[k + 1] - P.ov_gr[k]);
+    const int W = P.ov_ngr * P.ov_ng, ndx = P.ov_ndx, ng = P.ov_ng;
+    double e = 0.;
+#pragma unroll
+    for (int dm = 0; dm < 2; dm++)
+#pragma unroll
+        for (int dn = 0; dn < 2; dn++)
+#pragma unroll
+            for (int dk = 0; dk < 2; dk++)
+#pragma unroll
+                for (int dl = 0; dl < 2; dl++) {
+                    double wgt = (dl ? u : 1. - u) * (dk ? t : 1. - t) * (dn ? p : 1. - p) * (dm ? y : 1. - y);
+                    e += tab[(int64_t)((m + dm) * ndx + n + dn) * W + (k + dk) * ng + l + dl] * wgt;
+                }
+    return e > 1. ? 1. : (e < 0. ? 0. : e);
+}
+
+// ------------------------------------------------------------------------------
+// layer setup: iteration_scheme_lvg::set_parameters / set_gas_param
+// ------------------------------------------------------------------------------
+__device__ __forceinline__ void layer_setup(const LvgDevProblem &P, const LvgLaunch &Lc, int l, Smem &sm) {
+    const int t = threadIdx.x;
+    if (t == 0) {
+        const int64_t ld = Lc.soa_ld;
+        const double *s = Lc.soa + Lc.lay_offset + l;
+        double T = s[0 * ld], Te = s[1 * ld];
+        double ne = s[2 * ld], nh = s[3 * ld], nph2 = s[4 * ld], noh2 = s[5 * ld], nhe = s[6 * ld];
+        double vt = s[8 * ld];
+        sm.T = T; sm.Te = Te;
+        sm.nmol = s[7 * ld];
+        sm.ne = ne;
+        sm.vgrad = s[9 * ld];
+        sm.vw = sqrt(2. * BOLTZMANN_CONSTANT * T / P.mass + vt * vt);
+        for (int c = 0; c < P.nb_comp; c++) sm.dust[c] = s[(10 + c) * ld];
+        const double n5[5] = {nhe, nph2, noh2, nh, ne};
+        for (int k = 0; k < P.terms.nb_combos; k++) {
+            double a = 0.;
+            bool first = true;
+            for (int q = 0; q < 5; q++) {
+                double w = P.terms.combo_w[k][q];
+                if (w == 0.) continue;
+                double term = (w == 1.) ? n5[q] : w * n5[q];
+                a = first ? term : a + term;
+                first = false;
+            }
+            sm.cc[k] = a;
+        }
+        for (int tb = 0; tb < P.nb_tables; tb++) {
+            const double *tg = P.tab_tgrid + P.tab_tg_off[tb];
+            int jm = P.tab_jmax[tb];
+            double temp = (tb < P.nb_neutral) ? T : Te;
+            int lo = 0, hi = jm - 1;                  // collision_data::locate, strict '<'
+            while (hi - lo > 1) {
+                int j = lo + ((hi - lo) >> 1);
+                if (tg[j] < temp) lo = j; else hi = j;
+            }
+            sm.lo[tb] = lo;
+            double tmax = tg[jm - 1];
+            sm.teff[tb] = temp < tmax ? temp : tmax;
+        }
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ double table_rate(const LvgDevProblem &P, const Smem &sm, int tb, int pair) {
+    const int lo = sm.lo[tb];
+    const int64_t imax = (int64_t)P.tab_nb_lev[tb] * (P.tab_nb_lev[tb] - 1) / 2;
+    const double *c = P.tab_coeff + P.tab_c_off[tb];
+    const double *tg = P.tab_tgrid + P.tab_tg_off[tb];
+    double c0 = c[(int64_t)lo * imax + pair], c1 = c[(int64_t)(lo + 1) * imax + pair];
+    double deriv = (c1 - c0) / (tg[lo + 1] - tg[lo]);
+    return c0 + deriv * (sm.teff[tb] - tg[lo]);
+}
+
+// Collision operator K (with electrons; iteration_lvg.cpp:118-131) and the
+// boundary-layer matrix B (neutrals + A/2; iteration_control.cpp:69-85), both
+// stored row-major M[final][initial]; diagonals = minus column sums.
+__device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P, Smem &sm, double *K, double *B) {
+    const int N = P.N, t = threadIdx.x;
+    const double T = sm.T, Te = sm.Te;
+    for (int f = 1; f < N; f++) {
+        const int base = f * (f - 1) / 2;
+        for (int s = t; s < f; s += BT) {
+            const int pair = base + s;
+            const int cls = P.pair_class[pair];
+            double dn = 0.;
+#pragma unroll
+            for (int k = 0; k < LVG_MAX_TERMS; k++) {
+                int tb = P.terms.table[cls][k];
+                if (tb < 0) break;
+                double r = table_rate(P, sm, tb, pair) * sm.cc[P.terms.combo[cls][k]];
+                dn = (k == 0) ? r : dn + r;
+            }
+            const double de = P.energy[s] - P.energy[f];
+            double un = 0.;
+            if (dn > MIN_COLLISION_RATE) un = dn * exp(de * CM_INVERSE_TO_KELVINS / T) * P.g[f] / P.g[s];
+            else dn = 0.;
+            double dE = 0., uE = 0.;
+            int et = P.terms.etable[cls];
+            if (et >= 0) {
+                dE = table_rate(P, sm, et, pair) * sm.ne;
+                if (dE > MIN_COLLISION_RATE) uE = dE * exp(de * CM_INVERSE_TO_KELVINS / Te) * P.g[f] / P.g[s];
+                else dE = 0.;
+            }
+            K[s * N + f] = dn + dE;
+            K[f * N + s] = un + uE;
+            if (B) {
+                B[s * N + f] = 0.5 * P.einst[f * N + s] + dn;
+                B[f * N + s] = un;
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = t; i < N; i += BT) {
+        double a = 0., b = 0.;
+        for (int r = 0; r < N; r++) {
+            if (r == i) continue;
+            a += K[r * N + i];
+            if (B) b += B[r * N + i];
+        }
+        K[i * N + i] = -a;
+        if (B) B[i * N + i] = -b;
+    }
+    __syncthreads();
+    if (B) {
+        for (int j = t; j < N; j += BT) B[j] = 1.;   // row 0 <- 1
+    }
+    __syncthreads();
+}
+
+// ------------------------------------------------------------------------------
+// radiative terms: intensity_calc (iteration_lvg.cpp:163-185, :428-501)
+// ------------------------------------------------------------------------------
+__device__ __forceinline__ double dust_opacity(const LvgDevProblem &P, const LvgModeLines &M, const Smem &sm, int n) {
+    double a = 0.;
+    for (int c = 0; c < P.nb_comp; c++) a += M.line_sigma[(int64_t)c * M.nb_lines + n] * sm.dust[c];
+    return a;
+}
+
+__device__ __forceinline__ double intensity_single(const LvgDevProblem &P, const LvgModeLines &M, const Smem &sm, int n,
+                                   const double *pop) {
+    const int u = M.line_u[n], l = M.line_l[n];
+    const double energy = M.line_e[n];
+    const double c = sm.nmol / (EIGHT_PI * sm.vw * energy * energy * energy);
+    const double emiss = c * M.line_aul[n] * pop[u];
+    double opac = c * M.line_alu[n] * pop[l] - emiss + MIN_LINE_OPACITY;
+    if (opac < 0.) opac *= INV_TRANS_FACTOR;
+    const double dop = dust_opacity(P, M, sm, n);
+    const double avg = fabs(sm.vgrad);
+    const double gamma = avg / (sm.vw * opac);
+    const double delta = avg / (sm.vw * dop);
+    return emiss / opac * esc_func(P, gamma, delta);
+}
+
+__device__ __forceinline__ void intensity_pair(const LvgDevProblem &P, const LvgModeLines &M, const Smem &sm, int n1, int n2,
+                               const double *pop, double &i1, double &i2) {
+    const double max_dx = 4.;
+    const int u1 = M.line_u[n1], l1 = M.line_l[n1], u2 = M.line_u[n2], l2 = M.line_l[n2];
+    const double energy = M.line_e[n1];
+    double c = sm.nmol / (EIGHT_PI * sm.vw * energy * energy * energy);
+    const double em1 = c * M.line_aul[n1] * pop[u1];
+    double op1 = c * (M.line_alu[n1] * pop[l1] - M.line_aul[n1] * pop[u1]) + MIN_LINE_OPACITY;
+    const double em2 = c * M.line_aul[n2] * pop[u2];
+    double op2 = c * (M.line_alu[n2] * pop[l2] - M.line_aul[n2] * pop[u2]) + MIN_LINE_OPACITY;
+    if (op1 < 0.) op1 *= INV_TRANS_FACTOR;
+    if (op2 < 0.) op2 *= INV_TRANS_FACTOR;
+    const double avg = fabs(sm.vgrad);
+    const double g1 = avg / (sm.vw * op1), g2 = avg / (sm.vw * op2);
+    const double delta = avg / (sm.vw * dust_opacity(P, M, sm, n1));
+    double dx = (P.energy[u1] - P.energy[l1] - P.energy[u2] + P.energy[l2]) * SPEED_OF_LIGHT / (energy * sm.vw);
+    if (sm.vgrad < 0.) dx *= -1.;
+    const double adx = fabs(dx);
+    double ep1 = 0., ep2 = 0., ep01 = 0., ep02 = 0.;
+    if (adx < max_dx) {
+        ep1 = overlap_esc_func(P, P.ov_p1, g1, delta, g2 / g1, dx);
+        ep2 = overlap_esc_func(P, P.ov_p1, g2, delta, g1 / g2, -dx);
+    }
+    if (adx > max_dx - 0.5) {
+        ep01 = esc_func(P, g1, delta);
+        ep02 = esc_func(P, g2, delta);
+    }
+    if (adx > max_dx) { ep1 = ep01; ep2 = ep02; }
+    else if (adx > max_dx - 0.5) {
+        c = 2. * (max_dx - adx);
+        ep1 = ep01 * (1. - c) + ep1 * c;
+        ep2 = ep02 * (1. - c) + ep2 * c;
+    }
+    i1 = em1 / op1 * ep1;
+    i2 = em2 / op2 * ep2;
+    if (adx < max_dx) {
+        ep1 = overlap_esc_func(P, P.ov_p2, g1, delta, g2 / g1, dx);
+        ep2 = overlap_esc_func(P, P.ov_p2, g2, delta, g1 / g2, -dx);
+        if (adx > max_dx - 0.5) {
+            c = 2. * (max_dx - adx);
+            ep1 *= c; ep2 *= c;
+        }
+        i1 += em2 / op2 * ep1;
+        i2 += em1 / op1 * ep2;
+    }
+}
+
+// y[2n] = A_ul(1+I), y[2n+1] = A_lu*I for every line of the mode
+__device__ __forceinline__ void compute_line_terms(const LvgDevProblem &P, const LvgModeLines &M, const Smem &sm,
+                                   const double *pop, double *y) {
+    for (int q = threadIdx.x; q < M.nb_units; q += BT) {
+        int n1 = M.unit_l0[q], n2 = M.unit_l1[q];
+        if (n2 < 0) {
+            double I = intensity_single(P, M, sm, n1, pop);
+            y[2 * n1] = M.line_aul[n1] * (1. + I);
+            y[2 * n1 + 1] = M.line_alu[n1] * I;
+        } else {
+            double i1, i2;
+            intensity_pair(P, M, sm, n1, n2, pop, i1, i2);
+            y[2 * n1] = M.line_aul[n1] * (1. + i1);
+            y[2 * n1 + 1] = M.line_alu[n1] * i1;
+            y[2 * n2] = M.line_aul[n2] * (1. + i2);
+            y[2 * n2 + 1] = M.line_alu[n2] * i2;
+        }
+    }
+}
+
+// A = K + radiative terms, row 0 <- 1 (iteration_lvg.cpp:117-151), then
+// df = e0 - A n (:153-160); returns eq_error = max |df| (:103-107).
+__device__ __forceinline__ double assemble_and_residual(const LvgDevProblem &P, const LvgModeLines &M, const double *K, double *A,
+                                        const double *y, const double *pop, double *df, Smem &sm) {
+    const int N = P.N, t = threadIdx.x;
+    // 1) copy K -> A (row 0 = ones)
+    const int NN = N * N;
+    for (int e = t; e < NN; e += BT) A[e] = (e < N) ? 1. : K[e];
+    __syncthreads();
+    // 2) off-diagonal radiative terms: M[l][u] += y1, M[u][l] += y2 (row 0 skipped: overwritten by ones)
+    for (int n = t; n < M.nb_lines; n += BT) {
+        int u = M.line_u[n], l = M.line_l[n];
+        if (l != 0) A[l * N + u] += y[2 * n];
+        A[u * N + l] += y[2 * n + 1];
+    }
+    // 3) diagonal: subtract every contribution of the level in CSR order
+    for (int i = t; i < N; i += BT) {
+        if (i == 0) continue;
+        double a = A[i * N + i];
+        for (int e = M.diag_ptr[i]; e < M.diag_ptr[i + 1]; e++) a -= y[M.diag_ent[e]];
+        A[i * N + i] = a;
+    }
+    __syncthreads();
+    // 4) residual, one wave per row
+    const int w = t >> 6, lane = t & 63;
+    double emax = 0.;
+    for (int i = w; i < N; i += NW) {
+        double s = 0.;
+        for (int j = lane; j < N; j += 64) s += A[i * N + j] * pop[j];
+        s = wave_sum(s);
+        double d = (i == 0 ? 1. : 0.) - s;
+        if (lane == 0) df[i] = d;
+        emax = fmax(emax, fabs(d));
+    }
+    return block_max(emax, sm);
+}
+
+// ------------------------------------------------------------------------------
+// blocked right-looking LU with partial pivoting, b solved alongside.
+// A: N x N row-major (lda = N) in the slot workspace; b: LDS [N]; on return b = x.
+// ------------------------------------------------------------------------------
+__device__ __forceinline__ void block_lu_solve(double *A, int N, double *b, Smem &sm) {
+    const int t = threadIdx.x;
+    for (int k0 = 0; k0 < N; k0 += NB) {
+        const int nb = min(NB, N - k0);
+        const int R = N - k0;
+        // ---- panel load (rows k0..N-1, cols k0..k0+nb-1)
+        for (int e = t; e < R * nb; e += BT) {
+            int r = e / nb, c = e - r * nb;
+            sm.pu.P[r][c] = A[(int64_t)(k0 + r) * N + k0 + c];
+        }
+        __syncthreads();
+        // ---- panel factorization
+        for (int c = 0; c < nb; c++) {
+            double v = -1.;
+            int idx = 0x7fffffff;
+            for (int r = c + t; r < R; r += BT) {
+                double a = fabs(sm.pu.P[r][c]);
+                if (a > v) { v = a; idx = r; }
+            }
+            int p = block_argmax(v, idx, sm);
+            if (p != c) {
+                for (int j = t; j < nb; j += BT) {
+                    double x = sm.pu.P[c][j]; sm.pu.P[c][j] = sm.pu.P[p][j]; sm.pu.P[p][j] = x;
+                }
+                if (t == 0) { double x = b[k0 + c]; b[k0 + c] = b[k0 + p]; b[k0 + p] = x; }
+            }
+            if (t == 0) sm.piv[c] = p;
+            __syncthreads();
+            const double piv = sm.pu.P[c][c];
+            const double bc = b[k0 + c];
+            for (int r = c + 1 + t; r < R; r += BT) {
+                double lr = sm.pu.P[r][c] / piv;
+                sm.pu.P[r][c] = lr;
+                for (int j = c + 1; j < nb; j++) sm.pu.P[r][j] -= lr * sm.pu.P[c][j];
+                b[k0 + r] -= lr * bc;
+            }
+            __syncthreads();
+        }
+        // ---- keep U11 in A (for back substitution), L11 and L21^T in LDS
+        for (int e = t; e < nb * nb; e += BT) {
+            int r = e / nb, c = e - r * nb;
+            double x = sm.pu.P[r][c];
+            if (c >= r) A[(int64_t)(k0 + r) * N + k0 + c] = x;
+            sm.L11[r][c] = (c < r) ? x : 0.;
+        }
+        for (int e = t; e < (R - nb) * nb; e += BT) {
+            int c = e / (R - nb), r = e - c * (R - nb);
+            sm.LT[c][r] = sm.pu.P[nb + r][c];
+        }
+        __syncthreads();
+        const int C2 = N - k0 - nb;
+        if (C2 > 0) {
+            // ---- row interchanges + TRSM on trailing columns (thread per column),
+            //      U12 = L11^-1 A12 formed in place in LDS
+            for (int jj = t; jj < C2; jj += BT) {
+                const int j = k0 + nb + jj;
+                for (int c = 0; c < nb; c++) {
+                    int p = sm.piv[c];
+                    if (p != c) {
+                        double x = A[(int64_t)(k0 + c) * N + j];
+                        A[(int64_t)(k0 + c) * N + j] = A[(int64_t)(k0 + p) * N + j];
+                        A[(int64_t)(k0 + p) * N + j] = x;
+                    }
+                }
+                for (int i = 0; i < nb; i++) {
+                    double s = A[(int64_t)(k0 + i) * N + j];
+                    for (int m = 0; m < i; m++) s -= sm.L11[i][m] * sm.pu.U[m][jj];
+                    sm.pu.U[i][jj] = s;
+                    A[(int64_t)(k0 + i) * N + j] = s;
+                }
+            }
+            __syncthreads();
+            // ---- trailing update A22 -= L21 * U12, 4x4 register tiles, 64x64 per pass
+            const int R2 = R - nb;
+            const int tr = t >> 4, tc = t & 15;
+            const int ntr = (R2 + 63) >> 6, ntc = (C2 + 63) >> 6;
+            for (int tile = 0; tile < ntr * ntc; tile++) {
+                const int ti = tile / ntc, tj = tile - ti * ntc;
+                const int r0 = ti * 64 + tr * 4, c0 = tj * 64 + tc * 4;
+                double acc[4][4];
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        int r = r0 + i, cc = c0 + j;
+                        acc[i][j] = (r < R2 && cc < C2) ? A[(int64_t)(k0 + nb + r) * N + k0 + nb + cc] : 0.;
+                    }
+                for (int c = 0; c < nb; c++) {
+                    double a[4], bb[4];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) a[i] = sm.LT[c][min(r0 + i, NMAX - 1)];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) bb[j] = sm.pu.U[c][min(c0 + j, NMAX - 1)];
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+#pragma unroll
+                        for (int j = 0; j < 4; j++) acc[i][j] -= a[i] * bb[j];
+                }
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        int r = r0 + i, cc = c0 + j;
+                        if (r < R2 && cc < C2) A[(int64_t)(k0 + nb + r) * N + k0 + nb + cc] = acc[i][j];
+                    }
+            }
+        }
+        __syncthreads();
+    }
+    // ---- back substitution U x = y, blocked by NB from the bottom: wave 0 solves
+    //      the diagonal block through LDS, then all threads update the rows above
+    const int nblk = (N + NB - 1) / NB;
+    for (int kb = nblk - 1; kb >= 0; kb--) {
+        const int k0 = kb * NB, nb = min(NB, N - k0);
+        for (int e = t; e < nb * nb; e += BT) {
+            int r = e / nb, c = e - r * nb;
+            sm.L11[r][c] = A[(int64_t)(k0 + r) * N + k0 + c];
+        }
+        __syncthreads();
+        if (t < 64) {
+            for (int m = nb - 1; m >= 0; m--) {
+                const double xm = b[k0 + m] / sm.L11[m][m];
+                __builtin_amdgcn_wave_barrier();
+                if (t < m) b[k0 + t] -= sm.L11[t][m] * xm;
+                else if (t == m) b[k0 + m] = xm;
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        __syncthreads();
+        for (int i = t; i < k0; i += BT) {
+            double s = b[i];
+            const double *row = A + (int64_t)i * N + k0;
+            for (int m = 0; m < nb; m++) s -= row[m] * b[k0 + m];
+            b[i] = s;
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------
+// iteration_control (iteration_control.h:84-242)
+// ------------------------------------------------------------------------------
+struct Ctl {
+    int acceleration, accel_start, accel_period, nb_prev, max_iter;
+    int iter_nb, nb_after_accel;
+    double best_eq, eq_error, pop_error, rel_error;
+    int hp, np, hr, nr;   // ring heads and sizes: prev_level_pop / residual_list
+};
+
+struct Slot {
+    double *K, *A, *prev, *res, *opt, *y, *given, *df;
+};
+
+__device__ __forceinline__ double *ring(double *base, int head, int i, int N) {
+    return base + (int64_t)((head + i) & (NHIST - 1)) * N;
+}
+
+// calc_new_pop (iteration_lvg.cpp:87-110): sm.pold -> sm.pnew, returns eq_error
+__device__ __forceinline__ double calc_new_pop(const LvgDevProblem &P, const LvgModeLines &M, Slot &S, Smem &sm) {
+    const int N = P.N, t = threadIdx.x;
+    compute_line_terms(P, M, sm, sm.pold, S.y);
+    __syncthreads();
+    double eq = assemble_and_residual(P, M, S.K, S.A, S.y, sm.pold, S.df, sm);
+    for (int i = t; i < N; i += BT) sm.bvec[i] = (i == 0) ? 1. : 0.;
+    __syncthreads();
+    block_lu_solve(S.A, N, sm.bvec, sm);
+    for (int i = t; i < N; i += BT) sm.pnew[i] = sm.bvec[i];
+    __syncthreads();
+    return eq;
+}
+
+// accel_step (iteration_control.h:139-193). Each of the nb_param*nb_param + nb_param
+// sums runs in one thread in the reference's k order; the small system is solved
+// by thread 0 exactly as the oracle does (partial pivoting, no FMA contraction).
+__device__ __forceinline__ void accel_step(Ctl &C, Slot &S, int N, Smem &sm) {
+    const int t = threadIdx.x;
+    const int np = C.nb_prev - 1;
+    const double *r0 = ring(S.res, C.hr, 0, N);
+    const double *p0 = ring(S.prev, C.hp, 0, N);
+    const int nsum = np * np + np;
+    if (t < nsum) {
+        int i, j;
+        if (t < np * np) { i = t / np; j = t - i * np; } else { i = t - np * np; j = -1; }
+        const double *ri = ring(S.res, C.hr, i + 1, N);
+        const double *rj = (j >= 0) ? ring(S.res, C.hr, j + 1, N) : nullptr;
+        double a = 0.;
+        for (int k = 0; k < N; k++) {
+            double w = __dadd_rn(p0[k], 1.e-99);
+            double ww = __dmul_rn(w, w);
+            double num = (j >= 0) ? __dmul_rn(__dsub_rn(r0[k], ri[k]), __dsub_rn(r0[k], rj[k]))
+                                  : __dmul_rn(__dsub_rn(r0[k], ri[k]), r0[k]);
+            a = __dadd_rn(a, num / ww);
+        }
+        sm.hist_acc[t] = a;
+    }
+    __syncthreads();
+    if (t == 0) {
+        double Am[4][4], bv[4];
+        for (int i = 0; i < np; i++) {
+            for (int j = 0; j < np; j++) Am[i][j] = sm.hist_acc[i * np + j];
+            bv[i] = sm.hist_acc[np * np + i];
+        }
+        for (int k = 0; k < np; k++) {
+            int p = k;
+            double amax = fabs(Am[k][k]);
+            for (int i = k + 1; i < np; i++) if (fabs(Am[i][k]) > amax) { amax = fabs(Am[i][k]); p = i; }
+            if (p != k) {
+                for (int j = 0; j < np; j++) { double x = Am[k][j]; Am[k][j] = Am[p][j]; Am[p][j] = x; }
+                double x = bv[k]; bv[k] = bv[p]; bv[p] = x;
+            }
+            double piv = Am[k][k];
+            for (int i = k + 1; i < np; i++) {
+                double l = Am[i][k] / piv;
+                Am[i][k] = l;
+                for (int j = k + 1; j < np; j++) Am[i][j] = __dsub_rn(Am[i][j], __dmul_rn(l, Am[k][j]));
+                bv[i] = __dsub_rn(bv[i], __dmul_rn(l, bv[k]));
+            }
+        }
+        for (int k = np - 1; k >= 0; k--) {
+            bv[k] /= Am[k][k];
+            double x = bv[k];
+            for (int i = 0; i < k; i++) bv[i] = __dsub_rn(bv[i], __dmul_rn(Am[i][k], x));
+        }
+        double sum = 0.;
+        for (int i = 0; i < np; i++) { sum = __dadd_rn(sum, bv[i]); sm.hist_acc[16 + i] = bv[i]; }
+        sm.hist_acc[31] = sum;
+    }
+    __syncthreads();
+    const double sum = sm.hist_acc[31];
+    for (int k = t; k < N; k += BT) {
+        double a = __dmul_rn(__dsub_rn(1., sum), p0[k]);
+        for (int i = 0; i < np; i++) a = __dadd_rn(a, __dmul_rn(sm.hist_acc[16 + i], ring(S.prev, C.hp, i + 1, N)[k]));
+        sm.pold[k] = a;
+    }
+    __syncthreads();
+}
+
+// next_step (iteration_control.h:84-137)
+__device__ __forceinline__ void next_step(Ctl &C, const LvgDevProblem &P, const LvgModeLines &M, Slot &S, Smem &sm) {
+    const int N = P.N, t = threadIdx.x;
+    // prev_level_pop.push_front(pop_old)
+    C.hp = (C.hp + NHIST - 1) & (NHIST - 1);
+    C.np++;
+    double *pf = ring(S.prev, C.hp, 0, N);
+    for (int i = t; i < N; i += BT) pf[i] = sm.pold[i];
+    __syncthreads();
+    if (C.acceleration && (C.iter_nb == C.accel_start || C.nb_after_accel == C.accel_period)) {
+        accel_step(C, S, N, sm);
+        C.nb_after_accel = 0;
+    }
+    C.eq_error = calc_new_pop(P, M, S, sm);
+    if (C.acceleration && C.iter_nb >= C.accel_start) C.nb_after_accel++;
+    const bool better = C.eq_error < C.best_eq;
+    if (better) C.best_eq = C.eq_error;
+    // residual_list.push_front(pop_new - pop_old)
+    C.hr = (C.hr + NHIST - 1) & (NHIST - 1);
+    C.nr++;
+    double *rf = ring(S.res, C.hr, 0, N);
+    double pe = 0., re = 0.;
+    for (int i = t; i < N; i += BT) {
+        double r = sm.pnew[i] - sm.pold[i];
+        rf[i] = r;
+        pe = fmax(pe, fabs(r));
+        re = fmax(re, fabs(r / (sm.pold[i] + 1.e-99)));
+        if (better) S.opt[i] = sm.pold[i];
+    }
+    C.pop_error = block_max(pe, sm);
+    C.rel_error = block_max(re, sm);
+    if (C.nr > C.nb_prev + 1) C.nr = C.nb_prev + 1;
+    if (C.np > C.nb_prev + 1) C.np = C.nb_prev + 1;
+    __syncthreads();
+    if (C.iter_nb < C.max_iter - 1) {
+        for (int i = t; i < N; i += BT) sm.pold[i] = sm.pnew[i];
+    } else {
+        for (int i = t; i < N; i += BT) sm.pold[i] = S.opt[i];
+        C.eq_error = C.best_eq;
+    }
+    C.iter_nb++;
+    __syncthreads();
+}
+
+// calculate_populations (iteration_control.h:196-242); pops in/out in sm.pold
+__device__ __forceinline__ bool calculate_populations(Ctl &C, const LvgDevProblem &P, const LvgModeLines &M, Slot &S, Smem &sm,
+                                      const LvgLaunch &Lc, int max_nb, int accel) {
+    const int N = P.N;
+    C.acceleration = accel;
+    C.accel_start = Lc.accel_start;
+    C.accel_period = Lc.accel_period;
+    C.nb_prev = Lc.accel_nb;
+    C.max_iter = max_nb;
+    C.iter_nb = C.nb_after_accel = 0;
+    C.best_eq = 1.;
+    C.eq_error = C.pop_error = C.rel_error = 0.;
+    C.hp = C.hr = 0;
+    C.np = C.nr = 0;
+    for (int i = threadIdx.x; i < N; i += BT) S.opt[i] = 0.;
+    __syncthreads();
+    bool found;
+    do {
+        next_step(C, P, M, S, sm);
+        found = C.rel_error < Lc.min_error;
+    } while (C.iter_nb < C.max_iter && !found);
+    return found;
+}
+
+__device__ __forceinline__ void boundary_layer_populations(const LvgDevProblem &P, Slot &S, Smem &sm) {
+    const int N = P.N, t = threadIdx.x;
+    for (int i = t; i < N; i += BT) sm.bvec[i] = (i == 0) ? 1. : 0.;
+    __syncthreads();
+    block_lu_solve(S.A, N, sm.bvec, sm);   // S.A holds the boundary matrix
+    for (int i = t; i < N; i += BT) sm.pold[i] = sm.bvec[i];
+    __syncthreads();
+}
+
+__device__ __forceinline__ Slot make_slot(const LvgDevProblem &P, const LvgLaunch &Lc, int slot) {
+    const int N = P.N;
+    double *w = Lc.ws + (int64_t)slot * Lc.ws_stride;
+    Slot S;
+    S.K = w; w += (int64_t)N * N;
+    S.A = w; w += (int64_t)N * N;
+    S.prev = w; w += (int64_t)NHIST * N;
+    S.res = w; w += (int64_t)NHIST * N;
+    S.opt = w; w += N;
+    S.given = w; w += N;
+    S.df = w; w += N;
+    S.y = w;
+    return S;
+}
+
+// One layer of calc_molecular_populations (radiative_transfer.cpp:236-288).
+__device__ __forceinline__ void solve_layer(const LvgDevProblem &P, const LvgLaunch &Lc, int l, Slot &S, Smem &sm) {
+    const int N = P.N, t = threadIdx.x;
+    const LvgModeLines &M = Lc.line_overlap ? P.overlap : P.plain;
+    layer_setup(P, Lc, l, sm);
+    double *pops = Lc.pops + (int64_t)l * N;
+    lvg_layer_status *st = reinterpret_cast<lvg_layer_status *>(Lc.status) + l;
+    const bool need_boundary = (Lc.init != LVG_INIT_GIVEN);
+    build_collision_operators(P, sm, S.K, need_boundary ? S.A : nullptr);
+
+    // initial guess
+    bool from_prev = false;
+    if (Lc.init == LVG_INIT_WARM_CHAIN && Lc.chain && (Lc.lay_offset + l) > 0) {
+        const lvg_layer_status *ps = reinterpret_cast<const lvg_layer_status *>(Lc.status) + l - 1;
+        from_prev = ps->converged != 0;
+    }
+    if (Lc.init == LVG_INIT_GIVEN) {
+        for (int i = t; i < N; i += BT) { sm.pold[i] = pops[i]; S.given[i] = pops[i]; }
+        __syncthreads();
+    } else if (from_prev) {
+        for (int i = t; i < N; i += BT) { sm.pold[i] = pops[i - N]; S.given[i] = pops[i - N]; }
+        __syncthreads();
+    } else {
+        boundary_layer_populations(P, S, sm);
+        for (int i = t; i < N; i += BT) S.given[i] = sm.pold[i];
+        __syncthreads();
+    }
+    if (Lc.dbg_mode == 2) {
+        for (int i = t; i < N; i += BT) pops[i] = sm.pold[i];
+        return;
+    }
+    Ctl C;
+    const int accel = Lc.acceleration;
+    bool found = calculate_populations(C, P, M, S, sm, Lc, accel ? Lc.max_iter_acc : Lc.max_iter_plain, accel);
+    int iters = C.iter_nb, retry = 0;
+    if (!found && accel && Lc.allow_plain_retry) {
+        for (int i = t; i < N; i += BT) sm.pold[i] = S.given[i];
+        __syncthreads();
+        found = calculate_populations(C, P, M, S, sm, Lc, Lc.max_iter_plain, 0);
+        iters += C.iter_nb;
+        retry = 1;
+    }
+    for (int i = t; i < N; i += BT) pops[i] = sm.pold[i];
+    if (t == 0) {
+        st->converged = found ? 1 : 0;
+        st->iterations = iters;
+        st->used_plain_retry = retry;
+        st->reserved = 0;
+        st->eq_error = C.eq_error;
+        st->rel_error = C.rel_error;
+        st->pop_error = C.pop_error;
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(BT, 2) solve_kernel(const LvgDevProblem *__restrict__ Pp,
+                                                       const LvgLaunch *__restrict__ Lp) {
+    __shared__ Smem sm;
+    const LvgDevProblem &P = *Pp;
+    const LvgLaunch &Lc = *Lp;
+    Slot S = make_slot(P, Lc, blockIdx.x);
+    for (;;) {
+        if (threadIdx.x == 0) sm.layer = atomicAdd(Lc.counter, 1);
+        __syncthreads();
+        const int l = sm.layer;
+        __syncthreads();
+        if (l >= Lc.nb_lay) break;
+        solve_layer(P, Lc, l, S, sm);
+    }
+}
+
+// lvg_debug_calc_new_pop: one calc_new_pop for one layer (block 0 only)
+__global__ void __launch_bounds__(BT, 2) debug_kernel(const LvgDevProblem *__restrict__ Pp,
+                                                       const LvgLaunch *__restrict__ Lp) {
+    __shared__ Smem sm;
+    const LvgDevProblem &P = *Pp;
+    const LvgLaunch &Lc = *Lp;
+    Slot S = make_slot(P, Lc, 0);
+    const int N = P.N, t = threadIdx.x;
+    const LvgModeLines &M = Lc.line_overlap ? P.overlap : P.plain;
+    layer_setup(P, Lc, 0, sm);
+    build_collision_operators(P, sm, S.K, nullptr);
+    for (int i = t; i < N; i += BT) sm.pold[i] = Lc.dbg_pop_in[i];
+    __syncthreads();
+    compute_line_terms(P, M, sm, sm.pold, S.y);
+    __syncthreads();
+    double eq = assemble_and_residual(P, M, S.K, S.A, S.y, sm.pold, S.df, sm);
+    for (int e = t; e < N * N; e += BT) Lc.dbg_matrix[e] = S.A[e];
+    for (int i = t; i < N; i += BT) { Lc.dbg_df[i] = S.df[i]; sm.bvec[i] = (i == 0) ? 1. : 0.; }
+    __syncthreads();
+    block_lu_solve(S.A, N, sm.bvec, sm);
+    for (int i = t; i < N; i += BT) Lc.pops[i] = sm.bvec[i];
+    if (t == 0) Lc.dbg_df[N] = eq;
+}
+
+}  // namespace lvg
+
+// P and L are DEVICE pointers to the parameter blocks
+extern "C" hipError_t lvg_launch_solve(const LvgDevProblem *P, const LvgLaunch *L, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(lvg::solve_kernel, dim3(grid), dim3(lvg::BT), 0, s, P, L);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t lvg_launch_debug(const LvgDevProblem *P, const LvgLaunch *L, hipStream_t s) {
+    hipLaunchKernelGGL(lvg::debug_kernel, dim3(1), dim3(lvg::BT), 0, s, P, L);
+    return hipGetLastError();
+}
+
+extern "C" int lvg_kernel_max_levels(void) { return lvg::NMAX; }
+extern "C" int lvg_kernel_block_threads(void) { return lvg::BT; }
+extern "C" hipError_t lvg_kernel_occupancy(int *blocks_per_cu) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, lvg::solve_kernel, lvg::BT, 0);
+}

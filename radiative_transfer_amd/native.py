@@ -1,0 +1,132 @@
+"""ctypes binding of liblvg_amd.so (the C ABI of include/lvg_amd.h).
+
+There is no CPU fallback: if the HIP library is missing or cannot load, every
+entry point raises. This is the same binding a maintainer would add on the
+reference side.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "_lib", "liblvg_amd.so")
+
+# every symbol include/lvg_amd.h declares
+EXPORTS = ("lvg_abi_version", "lvg_solve_opts_default", "lvg_create", "lvg_destroy", "lvg_last_error",
+           "lvg_nb_lev", "lvg_solve_layers", "lvg_layer_soa_rows", "lvg_solve_layers_device",
+           "lvg_debug_calc_new_pop", "lvg_boundary_layer_populations", "lvg_last_kernel_time")
+
+_lib = None
+
+
+class LvgError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load the library (no device work). Raises if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise LvgError(f"HIP library not built: {path} (run radiative_transfer_amd.build)")
+    L = C.CDLL(path)
+    vp, i, dp = C.c_void_p, C.c_int, C.POINTER(C.c_double)
+    L.lvg_abi_version.restype = i
+    L.lvg_solve_opts_default.argtypes = [vp]
+    L.lvg_create.argtypes = [vp, i, C.POINTER(vp)]
+    L.lvg_destroy.argtypes = [vp]
+    L.lvg_last_error.argtypes = [vp]
+    L.lvg_last_error.restype = C.c_char_p
+    L.lvg_nb_lev.argtypes = [vp]
+    L.lvg_solve_layers.argtypes = [vp, vp, dp, vp, vp]
+    L.lvg_layer_soa_rows.argtypes = [vp]
+    L.lvg_solve_layers_device.argtypes = [vp, i, vp, vp, vp, vp, vp]
+    L.lvg_debug_calc_new_pop.argtypes = [vp, vp, i, dp, i, dp, dp, dp, dp]
+    L.lvg_boundary_layer_populations.argtypes = [vp, vp, dp]
+    L.lvg_last_kernel_time.argtypes = [vp, dp, C.POINTER(C.c_int)]
+    _lib = L
+    return L
+
+
+class LvgSolver:
+    """One handle: the device-resident tables of one molecule (lvg_create).
+
+    Mirrors the reference object graph built before calc_molecular_populations
+    (energy_diagram, einstein_coeff, collisional_transitions, iteration_scheme_lvg).
+    """
+
+    def __init__(self, problem: abi.Problem, device: int = 0):
+        self.lib = load()
+        self.problem = problem
+        self.N = problem.mol.nb_lev
+        self._cp = problem.to_c()
+        h = C.c_void_p()
+        rc = self.lib.lvg_create(self._cp.ptr, device, C.byref(h))
+        if rc != 0:
+            raise LvgError(f"lvg_create failed ({rc}): {self.lib.lvg_last_error(None).decode()}")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.lvg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise LvgError(f"{what} failed ({rc}): {self.lib.lvg_last_error(self.h).decode()}")
+
+    def solve_layers(self, layers: abi.Layers, opts=None, pops=None):
+        """Batched calc_molecular_populations over host buffers -> (pops [L,N], status)."""
+        o = opts if opts is not None else abi.default_opts()
+        cl = layers.to_c()
+        out = np.zeros((layers.nb_lay, self.N)) if pops is None else np.array(pops, dtype=np.float64, copy=True)
+        st = np.zeros(layers.nb_lay, dtype=abi.STATUS_DTYPE)
+        rc = self.lib.lvg_solve_layers(self.h, cl.ptr, abi.dptr(out), C.byref(o), st.ctypes.data_as(C.c_void_p))
+        self._check(rc, "lvg_solve_layers")
+        return out, st
+
+    def soa_rows(self) -> int:
+        return self.lib.lvg_layer_soa_rows(self.h)
+
+    def solve_layers_device(self, nb_lay: int, soa_ptr: int, pops_ptr: int, status_ptr: int, opts=None,
+                            stream_ptr: int = 0):
+        """Device-resident variant: raw device pointers (e.g. torch tensor.data_ptr())."""
+        o = opts if opts is not None else abi.default_opts()
+        rc = self.lib.lvg_solve_layers_device(self.h, nb_lay, C.c_void_p(soa_ptr), C.c_void_p(pops_ptr),
+                                              C.byref(o), C.c_void_p(status_ptr),
+                                              C.c_void_p(stream_ptr) if stream_ptr else None)
+        self._check(rc, "lvg_solve_layers_device")
+
+    def last_kernel_time(self):
+        ms = C.c_double()
+        n = C.c_int()
+        self._check(self.lib.lvg_last_kernel_time(self.h, C.byref(ms), C.byref(n)), "lvg_last_kernel_time")
+        return ms.value, n.value
+
+    def debug_calc_new_pop(self, layers: abi.Layers, layer: int, pop_in, overlap: int = 0):
+        cl = layers.to_c()
+        pin = np.ascontiguousarray(pop_in, dtype=np.float64)
+        M = np.zeros((self.N, self.N)); df = np.zeros(self.N); pout = np.zeros(self.N); e = C.c_double()
+        rc = self.lib.lvg_debug_calc_new_pop(self.h, cl.ptr, layer, abi.dptr(pin), overlap, abi.dptr(M),
+                                             abi.dptr(df), abi.dptr(pout), C.byref(e))
+        self._check(rc, "lvg_debug_calc_new_pop")
+        return M, df, pout, e.value
+
+    def boundary_layer_populations(self, layers: abi.Layers):
+        cl = layers.to_c()
+        out = np.zeros((layers.nb_lay, self.N))
+        self._check(self.lib.lvg_boundary_layer_populations(self.h, cl.ptr, abi.dptr(out)),
+                    "lvg_boundary_layer_populations")
+        return out
