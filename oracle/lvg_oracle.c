@@ -19,8 +19,14 @@
  *   - constants.h: CODATA-2018 CGS values.
  * Arithmetic follows the reference's expression order; build with
  * -ffp-contract=off (no FMA contraction) so it is a faithful scalar restatement.
+ * Three deliberate, documented choices make the oracle and the GPU path agree
+ * bit for bit (DESIGN.md "Parity"): the LU updates use an explicit fused
+ * multiply-add (fma) — the absent library's rounding is unknown anyway; exp and
+ * log10 come from include/lvg_math.h (< 1-2 ulp from libm, identical on host and
+ * device); the thermal width uses sqrt(x) for the reference's pow(x, 0.5).
  */
 #include "lvg_oracle.h"
+#include "../include/lvg_math.h"
 
 #include <math.h>
 #include <stdlib.h>
@@ -83,15 +89,15 @@ int oracle_lu_solve(double *a, double *b, int n)
             double l = a[i * n + k] / piv;
             a[i * n + k] = l;
             for (int j = k + 1; j < n; j++)
-                a[i * n + j] -= l * a[k * n + j];
-            b[i] -= l * b[k];
+                a[i * n + j] = fma(-l, a[k * n + j], a[i * n + j]);
+            b[i] = fma(-l, b[k], b[i]);
         }
     }
     for (int k = n - 1; k >= 0; k--) {
         b[k] /= a[k * n + k];
         double x = b[k];
         for (int i = 0; i < k; i++)
-            b[i] -= a[i * n + k] * x;
+            b[i] = fma(-a[i * n + k], x, b[i]);
     }
     return sing ? -1 : 0;
 }
@@ -149,7 +155,7 @@ double oracle_overlap_esc_func(const lvg_overlap_table *T, double gamma, double 
 {
     int l, k, n, m;
     double u, t, p, y, escf;
-    delta = log10(delta);
+    delta = lvg_log10(delta);
     m = locate_index(T->log10_delta, T->nb_d, delta);
     l = locate_index(T->gamma, T->nb_g, gamma);
     k = locate_index(T->gratio, T->nb_gr, gamma_ratio);
@@ -285,7 +291,7 @@ static void get_rate_neutrals(const scheme_t *S, int up, int low, double *down_r
             d = KRATE(0, tn) * (c[0] + c[1] + 3. * c[2]);
         }
         if (d > MIN_COLLISION_RATE)
-            *up_rate = d * exp((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / tn) * M->g[up] / ((double)M->g[low]);
+            *up_rate = d * lvg_exp((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / tn) * M->g[up] / ((double)M->g[low]);
         else *up_rate = d = 0.;
         *down_rate = d;
         return;
@@ -296,7 +302,7 @@ static void get_rate_neutrals(const scheme_t *S, int up, int low, double *down_r
         else
             d = KRATE(1, tn) * c[1] + KRATE(4, tn) * c[4];
         if (d > MIN_COLLISION_RATE)
-            *up_rate = d * exp((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / tn) * M->g[up] / ((double)M->g[low]);
+            *up_rate = d * lvg_exp((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / tn) * M->g[up] / ((double)M->g[low]);
         else *up_rate = d = 0.;
         *down_rate = d;
         return;
@@ -311,7 +317,7 @@ static void get_rate_neutrals(const scheme_t *S, int up, int low, double *down_r
         if (up < tab[1].nb_lev)
             d += KRATE(1, tn) * c[1] + KRATE(2, tn) * c[2];
         if (d > MIN_COLLISION_RATE)
-            u = d * exp((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / tn) * M->g[up] / ((double)M->g[low]);
+            u = d * lvg_exp((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / tn) * M->g[up] / ((double)M->g[low]);
         else d = 0.;
         *down_rate = d; *up_rate = u;
         return;
@@ -320,7 +326,7 @@ static void get_rate_neutrals(const scheme_t *S, int up, int low, double *down_r
     for (int i = 0; i < C->nb_neutral; i++)
         if (up < tab[i].nb_lev) d += KRATE(i, tn) * c[i];
     if (d > MIN_COLLISION_RATE)
-        *up_rate = d * exp((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / tn) * M->g[up] / ((double)M->g[low]);
+        *up_rate = d * lvg_exp((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / tn) * M->g[up] / ((double)M->g[low]);
     else *up_rate = d = 0.;
     *down_rate = d;
 }
@@ -337,7 +343,7 @@ static void get_rate_electrons(const scheme_t *S, int up, int low, double *down_
         if (up < tab[i].nb_lev) { d = KRATE(i, te) * S->conc[i]; break; }
     }
     if (d > MIN_COLLISION_RATE)
-        *up_rate = d * exp((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / te) * M->g[up] / ((double)M->g[low]);
+        *up_rate = d * lvg_exp((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / te) * M->g[up] / ((double)M->g[low]);
     else *up_rate = d = 0.;
     *down_rate = d;
 }
@@ -359,7 +365,7 @@ static void scheme_set_layer(scheme_t *S, const lvg_layers *L, int l)
     S->temp_n = LAYER(temp_n);
     S->temp_el = LAYER(temp_el);
     S->mol_conc = LAYER(mol_conc);
-    S->vel_width = pow(2. * BOLTZMANN_CONSTANT * S->temp_n / S->P->mol->mass + LAYER(vel_turb) * LAYER(vel_turb), 0.5);
+    S->vel_width = sqrt(2. * BOLTZMANN_CONSTANT * S->temp_n / S->P->mol->mass + LAYER(vel_turb) * LAYER(vel_turb));
     set_gas_param(S, LAYER(temp_n), LAYER(temp_el), LAYER(he_conc), LAYER(ph2_conc), LAYER(oh2_conc),
                   LAYER(h_conc), LAYER(el_conc));
 }
@@ -960,3 +966,7 @@ int oracle_nb_overlap_lines(const lvg_problem *P, double vel_width, int *nb_doub
     }
     return LVG_OK;
 }
+
+/* probes of the shared elementary functions (tests compare them with libm) */
+double oracle_exp(double x) { return lvg_exp(x); }
+double oracle_log10(double x) { return lvg_log10(x); }

@@ -25,6 +25,8 @@ double oracle_overlap_esc_func(const lvg_overlap_table *T, double gamma, double 
                                double gamma_ratio, double delta_x);
 double oracle_dust_absorption(const lvg_dust *d, double energy, const double *conc);
 int    oracle_lu_solve(double *a, double *b, int n);
+double oracle_exp(double x);
+double oracle_log10(double x);
 #ifdef __cplusplus
 }
 #endif

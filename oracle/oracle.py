@@ -19,8 +19,17 @@ LIB_PATH = os.path.join(HERE, "_build", "liblvg_oracle.so")
 _lib = None
 
 
+def _stale() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    deps = [os.path.join(HERE, f) for f in ("lvg_oracle.c", "lvg_oracle.h", "Makefile")]
+    deps += [os.path.join(HERE, "..", "include", f) for f in ("lvg_amd.h", "lvg_math.h")]
+    return any(os.path.getmtime(x) > t for x in deps)
+
+
 def build(force: bool = False) -> str:
-    if force or not os.path.exists(LIB_PATH):
+    if force or _stale():
         subprocess.check_call(["make", "-s", "-C", HERE])
     return LIB_PATH
 
@@ -45,6 +54,10 @@ def lib():
         L.oracle_dust_absorption.argtypes = [vp, d, dp]
         L.oracle_dust_absorption.restype = d
         L.oracle_lu_solve.argtypes = [dp, dp, i]
+        L.oracle_exp.argtypes = [d]
+        L.oracle_exp.restype = d
+        L.oracle_log10.argtypes = [d]
+        L.oracle_log10.restype = d
         _lib = L
     return _lib
 

@@ -16,7 +16,8 @@ CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "_lib")
 LIB = os.path.join(LIB_DIR, "liblvg_amd.so")
 SOURCES = ["lvg_kernels.hip", "lvg_abi.cpp"]
-HEADERS = ["lvg_device.h", os.path.join("..", "..", "include", "lvg_amd.h")]
+HEADERS = ["lvg_device.h", os.path.join("..", "..", "include", "lvg_amd.h"),
+           os.path.join("..", "..", "include", "lvg_math.h")]
 ARCH = os.environ.get("LVG_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -33,7 +34,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return LIB
     os.makedirs(LIB_DIR, exist_ok=True)
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
            "-Wall", "-Wno-unused-function", "-o", LIB + ".tmp"]
     cmd += [os.path.join(CSRC, f) for f in SOURCES]
     if verbose:

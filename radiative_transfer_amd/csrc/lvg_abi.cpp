@@ -38,8 +38,9 @@ struct DevBuf {
 };
 
 struct ModeHost {
-    std::vector<int> u, l, unit0, unit1, dptr, dent;
+    std::vector<int> u, l, unit0, unit1, dptr, dent, cptr, cr, cy;
     std::vector<double> aul, alu, e, sigma;
+    int interleaved = 1;
 };
 
 }  // namespace
@@ -122,8 +123,10 @@ struct TermList {
     int table[LVG_MAX_TERMS];
     int combo[LVG_MAX_TERMS];
     int etable = -1;
+    int group = LVG_MAX_TERMS;
     bool operator<(const TermList &o) const {
         if (nt != o.nt) return nt < o.nt;
+        if (group != o.group) return group < o.group;
         for (int i = 0; i < nt; i++) {
             if (table[i] != o.table[i]) return table[i] < o.table[i];
             if (combo[i] != o.combo[i]) return combo[i] < o.combo[i];
@@ -205,7 +208,7 @@ int compile_rule(lvg_handle *h, const lvg_problem *prob, std::vector<uint8_t> &p
                 if (C.rule == LVG_COLL_OH && !covers(0, f))
                     return fail(h, LVG_E_ARG, "OH He table must cover all levels (read unchecked, coll_rates_oh.cpp:336)");
                 if (covers(0, f)) add(0, sp(HE));
-                if (covers(1, f)) { add(1, sp(PH2)); add(2, sp(OH2)); }
+                if (covers(1, f)) { tl.group = tl.nt; add(1, sp(PH2)); add(2, sp(OH2)); }
                 break;
             }
             case LVG_COLL_GENERIC: {                      // coll_rates.cpp:181-197
@@ -237,11 +240,13 @@ int compile_rule(lvg_handle *h, const lvg_problem *prob, std::vector<uint8_t> &p
     for (int c = 0; c < LVG_MAX_CLASSES; c++) {
         for (int k = 0; k < LVG_MAX_TERMS; k++) { tt.table[c][k] = -1; tt.combo[c][k] = 0; }
         tt.etable[c] = -1;
+        tt.group[c] = LVG_MAX_TERMS;
     }
     for (auto &kv : classes) {
         const TermList &tl = kv.first;
         for (int k = 0; k < tl.nt; k++) { tt.table[kv.second][k] = (int8_t)tl.table[k]; tt.combo[kv.second][k] = (int8_t)tl.combo[k]; }
         tt.etable[kv.second] = (int8_t)tl.etable;
+        tt.group[kv.second] = (int8_t)tl.group;
     }
     tt.nb_combos = (int)cb.w.size();
     for (size_t i = 0; i < cb.w.size(); i++)
@@ -266,18 +271,25 @@ void finish_mode(ModeHost &m, const lvg_problem *prob) {
     m.sigma.assign((size_t)std::max(1, nc) * std::max(1, nl), 0.);
     for (int c = 0; c < nc; c++)
         for (int n = 0; n < nl; n++) m.sigma[(size_t)c * nl + n] = dust_sigma(prob->dust->comp[c], m.e[n]);
-    std::vector<std::vector<int>> per(N);
+    std::vector<std::vector<int>> per(N);                 // line order
+    std::vector<std::vector<std::pair<int, int>>> col(N); // (partner level, y index)
     for (int n = 0; n < nl; n++) {
         per[m.u[n]].push_back(2 * n);
         per[m.l[n]].push_back(2 * n + 1);
+        col[m.u[n]].push_back({m.l[n], 2 * n});
+        col[m.l[n]].push_back({m.u[n], 2 * n + 1});
     }
     m.dptr.assign(N + 1, 0);
-    m.dent.clear();
+    m.cptr.assign(N + 1, 0);
     for (int i = 0; i < N; i++) {
         m.dptr[i] = (int)m.dent.size();
         for (int e : per[i]) m.dent.push_back(e);
+        std::sort(col[i].begin(), col[i].end());
+        m.cptr[i] = (int)m.cr.size();
+        for (auto &pr : col[i]) { m.cr.push_back(pr.first); m.cy.push_back(pr.second); }
     }
     m.dptr[N] = (int)m.dent.size();
+    m.cptr[N] = (int)m.cr.size();
 }
 
 // hfs_lines::sort / split (iteration_lvg.cpp:259-302), stale minimum kept (quirk q6)
@@ -304,6 +316,7 @@ struct Hfs {
 void build_overlap_mode(ModeHost &m, const lvg_problem *prob) {
     const lvg_molecule &M = *prob->mol;
     const int N = M.nb_lev;
+    m.interleaved = 0;
     auto group = [&](const Hfs &h, int start, int cnt) {
         int n0 = (int)m.u.size();
         add_line(m, prob, h.up[start], h.lo[start]);
@@ -357,6 +370,10 @@ int upload_mode(lvg_handle *h, const ModeHost &m, LvgModeLines &d) {
     if ((rc = upload(h, m.unit1.data(), m.unit1.size(), &d.unit_l1))) return rc;
     if ((rc = upload(h, m.dptr.data(), m.dptr.size(), &d.diag_ptr))) return rc;
     if ((rc = upload(h, m.dent.data(), m.dent.size(), &d.diag_ent))) return rc;
+    if ((rc = upload(h, m.cptr.data(), m.cptr.size(), &d.col_ptr))) return rc;
+    if ((rc = upload(h, m.cr.data(), m.cr.size(), &d.col_r))) return rc;
+    if ((rc = upload(h, m.cy.data(), m.cy.size(), &d.col_y))) return rc;
+    d.diag_interleaved = m.interleaved;
     return LVG_OK;
 }
 

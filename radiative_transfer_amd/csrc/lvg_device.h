@@ -26,6 +26,8 @@ struct LvgTermTable {
     int8_t table[LVG_MAX_CLASSES][LVG_MAX_TERMS];  // neutral terms, -1 = none
     int8_t combo[LVG_MAX_CLASSES][LVG_MAX_TERMS];
     int8_t etable[LVG_MAX_CLASSES];                // first applicable electron table, -1 = none
+    int8_t group[LVG_MAX_CLASSES];                 // terms [group, nt) are summed first, then added
+                                                   // (coll_rates_oh.cpp:341: d += k1*c1 + k2*c2)
     double combo_w[LVG_MAX_COMBOS][5];             // combo = sum_s w[s] * n[s] (he, ph2, oh2, h, e)
     int    nb_combos;
 };
@@ -36,8 +38,18 @@ struct LvgModeLines {          // one radiative scheme (plain LVG or line overla
     const double *line_aul, *line_alu, *line_e;
     const double *line_sigma;  // [nb_comp][nb_lines] dust cross section at the line energy
     const int    *unit_l0, *unit_l1;   // unit -> line index (l1 = -1 for a single line)
-    const int    *diag_ptr;    // [N+1]
-    const int    *diag_ent;    // line*2 + role (0: level is upper -> y1, 1: lower -> y2)
+    // per level d, radiative partners r sorted ascending: column d of the rate matrix
+    // gets +y at row r and the diagonal gets -y (y index = line*2 + role,
+    // role 0: d is the upper level -> y1 = A_ul(1+I); role 1: lower -> y2 = A_lu I)
+    const int    *col_ptr;     // [N+1]
+    const int    *col_r;
+    const int    *col_y;
+    // diagonal order: interleaved with the collision terms (plain scheme,
+    // iteration_lvg.cpp:118-147) or after all of them in line order (overlap
+    // scheme, iteration_lvg.cpp:354-412)
+    int           diag_interleaved;
+    const int    *diag_ptr;    // [N+1], line order (overlap scheme)
+    const int    *diag_ent;
 };
 
 struct LvgDevProblem {

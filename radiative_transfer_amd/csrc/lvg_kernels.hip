@@ -11,18 +11,35 @@
 // The grid is persistent: blocks pull layers from an atomic work queue, so
 // layers with very different iteration counts balance across CUs, and each
 // block's scratch (collision operator K, working matrix A, Ng history) lives in
-// a per-slot HBM workspace that stays L2/MALL resident while the slot works.
+// a per-slot HBM workspace.
 //
-// fp64 throughout, no MFMA: the dense work is a batched small LU (blocked,
-// right-looking, NB-wide panels in LDS, 4x4 register-tiled trailing update).
+// fp64 throughout, no MFMA. Bit-exact with the CPU oracle by construction: this
+// file is compiled with -ffp-contract=off, every operation follows the oracle's
+// order, and the only fused multiply-adds are the explicit fma() of the LU,
+// whose per-element update sequence (k ascending) the blocked factorization
+// preserves.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
 
 #include "lvg_device.h"
 #include "../../include/lvg_amd.h"
+#include "../../include/lvg_math.h"
 
 namespace lvg {
+
+// Diagnostic build only (-DLVG_PHASE_TIMERS): per-phase s_memtime cycle sums,
+// thread 0 of every block, flushed to lvg_phase_cycles[]. Never in the product .so.
+#ifdef LVG_PHASE_TIMERS
+enum { PH_SETUP, PH_BOUNDARY, PH_LINES, PH_ASSEMBLE, PH_PANEL, PH_TRSM, PH_GEMM, PH_BACKSUB, PH_CTL, PH_N };
+__device__ unsigned long long lvg_phase_cycles[16];
+#define TSTAMP(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#define TACC(ph, v0) do { if (threadIdx.x == 0) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    atomicAdd(&lvg_phase_cycles[ph], t_ - (v0)); } } while (0)
+#else
+#define TSTAMP(v) do {} while (0)
+#define TACC(ph, v0) do {} while (0)
+#endif
 
 constexpr int BT   = 256;   // threads per workgroup
 constexpr int NW   = BT / 64;
@@ -62,19 +79,12 @@ struct Smem {
 // ------------------------------------------------------------------------------
 // small helpers
 // ------------------------------------------------------------------------------
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
     return v;
 }
 
-// block max of a non-negative quantity (NaN-propagating like the reference's
-// "if (e < x) e = x" scan is not needed: inputs are finite in practice)
 __device__ __forceinline__ double block_max(double v, Smem &sm) {
     const int t = threadIdx.x, w = t >> 6;
     v = wave_max(v);
@@ -139,10 +149,11 @@ __device__ __forceinline__ double esc_func(const LvgDevProblem &P, double gamma,
     return e > 1. ? 1. : (e < 0. ? 0. : e);
 }
 
-// lvg_line_overlap_data::get_esc_func (lvg_method_functions.cpp:324-392)
-__device__ __forceinline__ double overlap_esc_func(const LvgDevProblem &P, const double *tab, double gamma, double delta,
-                                   double gratio, double dxv) {
-    delta = log10(delta);
+// lvg_line_overlap_data::get_esc_func (lvg_method_functions.cpp:324-392); the
+// 16 terms in the reference's order, each weighted (u, t, p, y) left to right
+__device__ __forceinline__ double overlap_esc_func(const LvgDevProblem &P, const double *tab, double gamma,
+                                                   double delta, double gratio, double dxv) {
+    delta = lvg_log10(delta);
     int m = locate_index(P.ov_ld, P.ov_nd, delta);
     int l = locate_index(P.ov_g, P.ov_ng, gamma);
     int k = locate_index(P.ov_gr, P.ov_ngr, gratio);
@@ -169,10 +180,9 @@ __device__ __forceinline__ double overlap_esc_func(const LvgDevProblem &P, const
 #pragma unroll
             for (int dk = 0; dk < 2; dk++)
 #pragma unroll
-                for (int dl = 0; dl < 2; dl++) {
-                    double wgt = (dl ? u : 1. - u) * (dk ? t : 1. - t) * (dn ? p : 1. - p) * (dm ? y : 1. - y);
-                    e += tab[(int64_t)((m + dm) * ndx + n + dn) * W + (k + dk) * ng + l + dl] * wgt;
-                }
+                for (int dl = 0; dl < 2; dl++)
+                    e += tab[(int64_t)((m + dm) * ndx + n + dn) * W + (k + dk) * ng + l + dl]
+                         * (dl ? u : 1. - u) * (dk ? t : 1. - t) * (dn ? p : 1. - p) * (dm ? y : 1. - y);
     return e > 1. ? 1. : (e < 0. ? 0. : e);
 }
 
@@ -191,7 +201,7 @@ __device__ __forceinline__ void layer_setup(const LvgDevProblem &P, const LvgLau
         sm.nmol = s[7 * ld];
         sm.ne = ne;
         sm.vgrad = s[9 * ld];
-        sm.vw = sqrt(2. * BOLTZMANN_CONSTANT * T / P.mass + vt * vt);
+        sm.vw = sqrt(2. * BOLTZMANN_CONSTANT * T / P.mass + vt * vt);   // iteration_lvg.cpp:65
         for (int c = 0; c < P.nb_comp; c++) sm.dust[c] = s[(10 + c) * ld];
         const double n5[5] = {nhe, nph2, noh2, nh, ne};
         for (int k = 0; k < P.terms.nb_combos; k++) {
@@ -223,6 +233,7 @@ __device__ __forceinline__ void layer_setup(const LvgDevProblem &P, const LvgLau
     __syncthreads();
 }
 
+// collision_data::get_rate (coll_rates.cpp:54-69), T-major table
 __device__ __forceinline__ double table_rate(const LvgDevProblem &P, const Smem &sm, int tb, int pair) {
     const int lo = sm.lo[tb];
     const int64_t imax = (int64_t)P.tab_nb_lev[tb] * (P.tab_nb_lev[tb] - 1) / 2;
@@ -233,9 +244,11 @@ __device__ __forceinline__ double table_rate(const LvgDevProblem &P, const Smem 
     return c0 + deriv * (sm.teff[tb] - tg[lo]);
 }
 
-// Collision operator K (with electrons; iteration_lvg.cpp:118-131) and the
-// boundary-layer matrix B (neutrals + A/2; iteration_control.cpp:69-85), both
-// stored row-major M[final][initial]; diagonals = minus column sums.
+// Collision operator K (neutral + electron rates; iteration_lvg.cpp:121-131) and
+// the boundary-layer matrix B (neutrals + A/2; iteration_control.cpp:69-85),
+// row-major M[final][initial]. K keeps off-diagonals only (its diagonal is
+// rebuilt every iteration in the reference's order); B gets its diagonal as the
+// ascending column sum, row 0 <- 1.
 __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P, Smem &sm, double *K, double *B) {
     const int N = P.N, t = threadIdx.x;
     const double T = sm.T, Te = sm.Te;
@@ -244,23 +257,27 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
         for (int s = t; s < f; s += BT) {
             const int pair = base + s;
             const int cls = P.pair_class[pair];
-            double dn = 0.;
+            const int grp = P.terms.group[cls];
+            double dn = 0., gsum = 0.;
+            int ng = 0;
 #pragma unroll
             for (int k = 0; k < LVG_MAX_TERMS; k++) {
                 int tb = P.terms.table[cls][k];
                 if (tb < 0) break;
                 double r = table_rate(P, sm, tb, pair) * sm.cc[P.terms.combo[cls][k]];
-                dn = (k == 0) ? r : dn + r;
+                if (k < grp) dn = (k == 0) ? r : dn + r;
+                else { gsum = (ng == 0) ? r : gsum + r; ng++; }
             }
+            if (ng) dn = dn + gsum;
             const double de = P.energy[s] - P.energy[f];
             double un = 0.;
-            if (dn > MIN_COLLISION_RATE) un = dn * exp(de * CM_INVERSE_TO_KELVINS / T) * P.g[f] / P.g[s];
+            if (dn > MIN_COLLISION_RATE) un = dn * lvg_exp(de * CM_INVERSE_TO_KELVINS / T) * P.g[f] / P.g[s];
             else dn = 0.;
             double dE = 0., uE = 0.;
             int et = P.terms.etable[cls];
             if (et >= 0) {
                 dE = table_rate(P, sm, et, pair) * sm.ne;
-                if (dE > MIN_COLLISION_RATE) uE = dE * exp(de * CM_INVERSE_TO_KELVINS / Te) * P.g[f] / P.g[s];
+                if (dE > MIN_COLLISION_RATE) uE = dE * lvg_exp(de * CM_INVERSE_TO_KELVINS / Te) * P.g[f] / P.g[s];
                 else dE = 0.;
             }
             K[s * N + f] = dn + dE;
@@ -272,21 +289,17 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
         }
     }
     __syncthreads();
-    for (int i = t; i < N; i += BT) {
-        double a = 0., b = 0.;
-        for (int r = 0; r < N; r++) {
-            if (r == i) continue;
-            a += K[r * N + i];
-            if (B) b += B[r * N + i];
-        }
-        K[i * N + i] = -a;
-        if (B) B[i * N + i] = -b;
-    }
-    __syncthreads();
     if (B) {
-        for (int j = t; j < N; j += BT) B[j] = 1.;   // row 0 <- 1
+        for (int d = t; d < N; d += BT) {
+            double a = 0.;
+            for (int r = 0; r < N; r++)
+                if (r != d) a = a - B[r * N + d];
+            B[d * N + d] = a;
+        }
+        __syncthreads();
+        for (int j = t; j < N; j += BT) B[j] = 1.;   // row 0 <- 1 (iteration_control.cpp:82-84)
+        __syncthreads();
     }
-    __syncthreads();
 }
 
 // ------------------------------------------------------------------------------
@@ -298,8 +311,8 @@ __device__ __forceinline__ double dust_opacity(const LvgDevProblem &P, const Lvg
     return a;
 }
 
-__device__ __forceinline__ double intensity_single(const LvgDevProblem &P, const LvgModeLines &M, const Smem &sm, int n,
-                                   const double *pop) {
+__device__ __forceinline__ double intensity_single(const LvgDevProblem &P, const LvgModeLines &M, const Smem &sm,
+                                                   int n, const double *pop) {
     const int u = M.line_u[n], l = M.line_l[n];
     const double energy = M.line_e[n];
     const double c = sm.nmol / (EIGHT_PI * sm.vw * energy * energy * energy);
@@ -307,14 +320,13 @@ __device__ __forceinline__ double intensity_single(const LvgDevProblem &P, const
     double opac = c * M.line_alu[n] * pop[l] - emiss + MIN_LINE_OPACITY;
     if (opac < 0.) opac *= INV_TRANS_FACTOR;
     const double dop = dust_opacity(P, M, sm, n);
-    const double avg = fabs(sm.vgrad);
-    const double gamma = avg / (sm.vw * opac);
-    const double delta = avg / (sm.vw * dop);
+    const double gamma = fabs(sm.vgrad) / (sm.vw * opac);
+    const double delta = fabs(sm.vgrad) / (sm.vw * dop);
     return emiss / opac * esc_func(P, gamma, delta);
 }
 
-__device__ __forceinline__ void intensity_pair(const LvgDevProblem &P, const LvgModeLines &M, const Smem &sm, int n1, int n2,
-                               const double *pop, double &i1, double &i2) {
+__device__ __forceinline__ void intensity_pair(const LvgDevProblem &P, const LvgModeLines &M, const Smem &sm,
+                                               int n1, int n2, const double *pop, double &i1, double &i2) {
     const double max_dx = 4.;
     const int u1 = M.line_u[n1], l1 = M.line_l[n1], u2 = M.line_u[n2], l2 = M.line_l[n2];
     const double energy = M.line_e[n1];
@@ -325,34 +337,32 @@ __device__ __forceinline__ void intensity_pair(const LvgDevProblem &P, const Lvg
     double op2 = c * (M.line_alu[n2] * pop[l2] - M.line_aul[n2] * pop[u2]) + MIN_LINE_OPACITY;
     if (op1 < 0.) op1 *= INV_TRANS_FACTOR;
     if (op2 < 0.) op2 *= INV_TRANS_FACTOR;
-    const double avg = fabs(sm.vgrad);
-    const double g1 = avg / (sm.vw * op1), g2 = avg / (sm.vw * op2);
-    const double delta = avg / (sm.vw * dust_opacity(P, M, sm, n1));
+    const double g1 = fabs(sm.vgrad) / (sm.vw * op1), g2 = fabs(sm.vgrad) / (sm.vw * op2);
+    const double delta = fabs(sm.vgrad) / (sm.vw * dust_opacity(P, M, sm, n1));
     double dx = (P.energy[u1] - P.energy[l1] - P.energy[u2] + P.energy[l2]) * SPEED_OF_LIGHT / (energy * sm.vw);
     if (sm.vgrad < 0.) dx *= -1.;
-    const double adx = fabs(dx);
     double ep1 = 0., ep2 = 0., ep01 = 0., ep02 = 0.;
-    if (adx < max_dx) {
+    if (fabs(dx) < max_dx) {
         ep1 = overlap_esc_func(P, P.ov_p1, g1, delta, g2 / g1, dx);
         ep2 = overlap_esc_func(P, P.ov_p1, g2, delta, g1 / g2, -dx);
     }
-    if (adx > max_dx - 0.5) {
+    if (fabs(dx) > max_dx - 0.5) {
         ep01 = esc_func(P, g1, delta);
         ep02 = esc_func(P, g2, delta);
     }
-    if (adx > max_dx) { ep1 = ep01; ep2 = ep02; }
-    else if (adx > max_dx - 0.5) {
-        c = 2. * (max_dx - adx);
+    if (fabs(dx) > max_dx) { ep1 = ep01; ep2 = ep02; }
+    else if (fabs(dx) > max_dx - 0.5) {
+        c = 2. * (max_dx - fabs(dx));
         ep1 = ep01 * (1. - c) + ep1 * c;
         ep2 = ep02 * (1. - c) + ep2 * c;
     }
     i1 = em1 / op1 * ep1;
     i2 = em2 / op2 * ep2;
-    if (adx < max_dx) {
+    if (fabs(dx) < max_dx) {
         ep1 = overlap_esc_func(P, P.ov_p2, g1, delta, g2 / g1, dx);
         ep2 = overlap_esc_func(P, P.ov_p2, g2, delta, g1 / g2, -dx);
-        if (adx > max_dx - 0.5) {
-            c = 2. * (max_dx - adx);
+        if (fabs(dx) > max_dx - 0.5) {
+            c = 2. * (max_dx - fabs(dx));
             ep1 *= c; ep2 *= c;
         }
         i1 += em2 / op2 * ep1;
@@ -360,9 +370,9 @@ __device__ __forceinline__ void intensity_pair(const LvgDevProblem &P, const Lvg
     }
 }
 
-// y[2n] = A_ul(1+I), y[2n+1] = A_lu*I for every line of the mode
+// y[2n] = A_ul(1+I), y[2n+1] = A_lu*I for every line of the scheme
 __device__ __forceinline__ void compute_line_terms(const LvgDevProblem &P, const LvgModeLines &M, const Smem &sm,
-                                   const double *pop, double *y) {
+                                                   const double *pop, double *y) {
     for (int q = threadIdx.x; q < M.nb_units; q += BT) {
         int n1 = M.unit_l0[q], n2 = M.unit_l1[q];
         if (n2 < 0) {
@@ -380,39 +390,46 @@ __device__ __forceinline__ void compute_line_terms(const LvgDevProblem &P, const
     }
 }
 
-// A = K + radiative terms, row 0 <- 1 (iteration_lvg.cpp:117-151), then
-// df = e0 - A n (:153-160); returns eq_error = max |df| (:103-107).
-__device__ __forceinline__ double assemble_and_residual(const LvgDevProblem &P, const LvgModeLines &M, const double *K, double *A,
-                                        const double *y, const double *pop, double *df, Smem &sm) {
+// A = K + radiative terms, row 0 <- 1 (iteration_lvg.cpp:117-151), as ONE pass
+// over the columns of K (thread d owns column d: coalesced row sweeps). The
+// diagonal is accumulated in the reference's order: for partner levels r
+// ascending, -rate(d->r) then, if a line joins d and r, -y (plain scheme); or
+// all collision terms first and the lines after, in line order (overlap scheme).
+// Then df = e0 - A n row by row in the reference's j order (:153-160).
+__device__ __forceinline__ double assemble_and_residual(const LvgDevProblem &P, const LvgModeLines &M,
+                                                        const double *K, double *A, const double *y,
+                                                        const double *pop, double *df, Smem &sm) {
     const int N = P.N, t = threadIdx.x;
-    // 1) copy K -> A (row 0 = ones)
-    const int NN = N * N;
-    for (int e = t; e < NN; e += BT) A[e] = (e < N) ? 1. : K[e];
-    __syncthreads();
-    // 2) off-diagonal radiative terms: M[l][u] += y1, M[u][l] += y2 (row 0 skipped: overwritten by ones)
-    for (int n = t; n < M.nb_lines; n += BT) {
-        int u = M.line_u[n], l = M.line_l[n];
-        if (l != 0) A[l * N + u] += y[2 * n];
-        A[u * N + l] += y[2 * n + 1];
+    for (int d = t; d < N; d += BT) {
+        int e = M.col_ptr[d];
+        const int e1 = M.col_ptr[d + 1];
+        int nr = (e < e1) ? M.col_r[e] : N;
+        double a = 0.;
+        for (int r = 0; r < N; r++) {
+            if (r == d) continue;
+            double v = K[r * N + d];
+            a = a - v;
+            if (r == nr) {
+                const double yy = y[M.col_y[e]];
+                if (M.diag_interleaved) a = a - yy;
+                v = v + yy;
+                e++;
+                nr = (e < e1) ? M.col_r[e] : N;
+            }
+            A[r * N + d] = (r == 0) ? 1. : v;
+        }
+        if (!M.diag_interleaved)
+            for (int q = M.diag_ptr[d]; q < M.diag_ptr[d + 1]; q++) a = a - y[M.diag_ent[q]];
+        A[d * N + d] = (d == 0) ? 1. : a;
     }
-    // 3) diagonal: subtract every contribution of the level in CSR order
-    for (int i = t; i < N; i += BT) {
-        if (i == 0) continue;
-        double a = A[i * N + i];
-        for (int e = M.diag_ptr[i]; e < M.diag_ptr[i + 1]; e++) a -= y[M.diag_ent[e]];
-        A[i * N + i] = a;
-    }
     __syncthreads();
-    // 4) residual, one wave per row
-    const int w = t >> 6, lane = t & 63;
     double emax = 0.;
-    for (int i = w; i < N; i += NW) {
-        double s = 0.;
-        for (int j = lane; j < N; j += 64) s += A[i * N + j] * pop[j];
-        s = wave_sum(s);
-        double d = (i == 0 ? 1. : 0.) - s;
-        if (lane == 0) df[i] = d;
-        emax = fmax(emax, fabs(d));
+    for (int i = t; i < N; i += BT) {
+        double s = (i == 0) ? 1. : 0.;
+        const double *row = A + (int64_t)i * N;
+        for (int j = 0; j < N; j++) s = s - row[j] * pop[j];
+        df[i] = s;
+        emax = fmax(emax, fabs(s));
     }
     return block_max(emax, sm);
 }
@@ -420,10 +437,13 @@ __device__ __forceinline__ double assemble_and_residual(const LvgDevProblem &P, 
 // ------------------------------------------------------------------------------
 // blocked right-looking LU with partial pivoting, b solved alongside.
 // A: N x N row-major (lda = N) in the slot workspace; b: LDS [N]; on return b = x.
+// Every element receives fma(-l_ik, u_kj, a_ij) for k ascending, exactly the
+// sequence of the unblocked oracle (oracle_lu_solve).
 // ------------------------------------------------------------------------------
 __device__ __forceinline__ void block_lu_solve(double *A, int N, double *b, Smem &sm) {
     const int t = threadIdx.x;
     for (int k0 = 0; k0 < N; k0 += NB) {
+        TSTAMP(tp0);
         const int nb = min(NB, N - k0);
         const int R = N - k0;
         // ---- panel load (rows k0..N-1, cols k0..k0+nb-1)
@@ -454,8 +474,8 @@ __device__ __forceinline__ void block_lu_solve(double *A, int N, double *b, Smem
             for (int r = c + 1 + t; r < R; r += BT) {
                 double lr = sm.pu.P[r][c] / piv;
                 sm.pu.P[r][c] = lr;
-                for (int j = c + 1; j < nb; j++) sm.pu.P[r][j] -= lr * sm.pu.P[c][j];
-                b[k0 + r] -= lr * bc;
+                for (int j = c + 1; j < nb; j++) sm.pu.P[r][j] = fma(-lr, sm.pu.P[c][j], sm.pu.P[r][j]);
+                b[k0 + r] = fma(-lr, bc, b[k0 + r]);
             }
             __syncthreads();
         }
@@ -471,6 +491,8 @@ __device__ __forceinline__ void block_lu_solve(double *A, int N, double *b, Smem
             sm.LT[c][r] = sm.pu.P[nb + r][c];
         }
         __syncthreads();
+        TACC(PH_PANEL, tp0);
+        TSTAMP(tp1);
         const int C2 = N - k0 - nb;
         if (C2 > 0) {
             // ---- row interchanges + TRSM on trailing columns (thread per column),
@@ -487,12 +509,14 @@ __device__ __forceinline__ void block_lu_solve(double *A, int N, double *b, Smem
                 }
                 for (int i = 0; i < nb; i++) {
                     double s = A[(int64_t)(k0 + i) * N + j];
-                    for (int m = 0; m < i; m++) s -= sm.L11[i][m] * sm.pu.U[m][jj];
+                    for (int m = 0; m < i; m++) s = fma(-sm.L11[i][m], sm.pu.U[m][jj], s);
                     sm.pu.U[i][jj] = s;
                     A[(int64_t)(k0 + i) * N + j] = s;
                 }
             }
             __syncthreads();
+            TACC(PH_TRSM, tp1);
+            TSTAMP(tp2);
             // ---- trailing update A22 -= L21 * U12, 4x4 register tiles, 64x64 per pass
             const int R2 = R - nb;
             const int tr = t >> 4, tc = t & 15;
@@ -517,7 +541,7 @@ __device__ __forceinline__ void block_lu_solve(double *A, int N, double *b, Smem
 #pragma unroll
                     for (int i = 0; i < 4; i++)
 #pragma unroll
-                        for (int j = 0; j < 4; j++) acc[i][j] -= a[i] * bb[j];
+                        for (int j = 0; j < 4; j++) acc[i][j] = fma(-a[i], bb[j], acc[i][j]);
                 }
 #pragma unroll
                 for (int i = 0; i < 4; i++)
@@ -527,11 +551,15 @@ __device__ __forceinline__ void block_lu_solve(double *A, int N, double *b, Smem
                         if (r < R2 && cc < C2) A[(int64_t)(k0 + nb + r) * N + k0 + nb + cc] = acc[i][j];
                     }
             }
+            __syncthreads();
+            TACC(PH_GEMM, tp2);
         }
         __syncthreads();
     }
+    TSTAMP(tb0);
     // ---- back substitution U x = y, blocked by NB from the bottom: wave 0 solves
-    //      the diagonal block through LDS, then all threads update the rows above
+    //      the diagonal block through LDS, then all threads update the rows above;
+    //      every b[i] receives its updates for k descending, as in the oracle
     const int nblk = (N + NB - 1) / NB;
     for (int kb = nblk - 1; kb >= 0; kb--) {
         const int k0 = kb * NB, nb = min(NB, N - k0);
@@ -544,7 +572,7 @@ __device__ __forceinline__ void block_lu_solve(double *A, int N, double *b, Smem
             for (int m = nb - 1; m >= 0; m--) {
                 const double xm = b[k0 + m] / sm.L11[m][m];
                 __builtin_amdgcn_wave_barrier();
-                if (t < m) b[k0 + t] -= sm.L11[t][m] * xm;
+                if (t < m) b[k0 + t] = fma(-sm.L11[t][m], xm, b[k0 + t]);
                 else if (t == m) b[k0 + m] = xm;
                 __builtin_amdgcn_wave_barrier();
             }
@@ -553,11 +581,12 @@ __device__ __forceinline__ void block_lu_solve(double *A, int N, double *b, Smem
         for (int i = t; i < k0; i += BT) {
             double s = b[i];
             const double *row = A + (int64_t)i * N + k0;
-            for (int m = 0; m < nb; m++) s -= row[m] * b[k0 + m];
+            for (int m = nb - 1; m >= 0; m--) s = fma(-row[m], b[k0 + m], s);
             b[i] = s;
         }
         __syncthreads();
     }
+    TACC(PH_BACKSUB, tb0);
 }
 
 // ------------------------------------------------------------------------------
@@ -581,9 +610,13 @@ __device__ __forceinline__ double *ring(double *base, int head, int i, int N) {
 // calc_new_pop (iteration_lvg.cpp:87-110): sm.pold -> sm.pnew, returns eq_error
 __device__ __forceinline__ double calc_new_pop(const LvgDevProblem &P, const LvgModeLines &M, Slot &S, Smem &sm) {
     const int N = P.N, t = threadIdx.x;
+    TSTAMP(tl0);
     compute_line_terms(P, M, sm, sm.pold, S.y);
     __syncthreads();
+    TACC(PH_LINES, tl0);
+    TSTAMP(ta0);
     double eq = assemble_and_residual(P, M, S.K, S.A, S.y, sm.pold, S.df, sm);
+    TACC(PH_ASSEMBLE, ta0);
     for (int i = t; i < N; i += BT) sm.bvec[i] = (i == 0) ? 1. : 0.;
     __syncthreads();
     block_lu_solve(S.A, N, sm.bvec, sm);
@@ -594,7 +627,7 @@ __device__ __forceinline__ double calc_new_pop(const LvgDevProblem &P, const Lvg
 
 // accel_step (iteration_control.h:139-193). Each of the nb_param*nb_param + nb_param
 // sums runs in one thread in the reference's k order; the small system is solved
-// by thread 0 exactly as the oracle does (partial pivoting, no FMA contraction).
+// by thread 0 exactly as oracle_lu_solve does.
 __device__ __forceinline__ void accel_step(Ctl &C, Slot &S, int N, Smem &sm) {
     const int t = threadIdx.x;
     const int np = C.nb_prev - 1;
@@ -608,11 +641,9 @@ __device__ __forceinline__ void accel_step(Ctl &C, Slot &S, int N, Smem &sm) {
         const double *rj = (j >= 0) ? ring(S.res, C.hr, j + 1, N) : nullptr;
         double a = 0.;
         for (int k = 0; k < N; k++) {
-            double w = __dadd_rn(p0[k], 1.e-99);
-            double ww = __dmul_rn(w, w);
-            double num = (j >= 0) ? __dmul_rn(__dsub_rn(r0[k], ri[k]), __dsub_rn(r0[k], rj[k]))
-                                  : __dmul_rn(__dsub_rn(r0[k], ri[k]), r0[k]);
-            a = __dadd_rn(a, num / ww);
+            double w = p0[k] + 1.e-99;
+            double num = (j >= 0) ? (r0[k] - ri[k]) * (r0[k] - rj[k]) : (r0[k] - ri[k]) * r0[k];
+            a = a + num / (w * w);
         }
         sm.hist_acc[t] = a;
     }
@@ -635,24 +666,24 @@ __device__ __forceinline__ void accel_step(Ctl &C, Slot &S, int N, Smem &sm) {
             for (int i = k + 1; i < np; i++) {
                 double l = Am[i][k] / piv;
                 Am[i][k] = l;
-                for (int j = k + 1; j < np; j++) Am[i][j] = __dsub_rn(Am[i][j], __dmul_rn(l, Am[k][j]));
-                bv[i] = __dsub_rn(bv[i], __dmul_rn(l, bv[k]));
+                for (int j = k + 1; j < np; j++) Am[i][j] = fma(-l, Am[k][j], Am[i][j]);
+                bv[i] = fma(-l, bv[k], bv[i]);
             }
         }
         for (int k = np - 1; k >= 0; k--) {
             bv[k] /= Am[k][k];
             double x = bv[k];
-            for (int i = 0; i < k; i++) bv[i] = __dsub_rn(bv[i], __dmul_rn(Am[i][k], x));
+            for (int i = 0; i < k; i++) bv[i] = fma(-Am[i][k], x, bv[i]);
         }
         double sum = 0.;
-        for (int i = 0; i < np; i++) { sum = __dadd_rn(sum, bv[i]); sm.hist_acc[16 + i] = bv[i]; }
+        for (int i = 0; i < np; i++) { sum = sum + bv[i]; sm.hist_acc[16 + i] = bv[i]; }
         sm.hist_acc[31] = sum;
     }
     __syncthreads();
     const double sum = sm.hist_acc[31];
     for (int k = t; k < N; k += BT) {
-        double a = __dmul_rn(__dsub_rn(1., sum), p0[k]);
-        for (int i = 0; i < np; i++) a = __dadd_rn(a, __dmul_rn(sm.hist_acc[16 + i], ring(S.prev, C.hp, i + 1, N)[k]));
+        double a = (1. - sum) * p0[k];
+        for (int i = 0; i < np; i++) a = a + sm.hist_acc[16 + i] * ring(S.prev, C.hp, i + 1, N)[k];
         sm.pold[k] = a;
     }
     __syncthreads();
@@ -703,8 +734,8 @@ __device__ __forceinline__ void next_step(Ctl &C, const LvgDevProblem &P, const 
 }
 
 // calculate_populations (iteration_control.h:196-242); pops in/out in sm.pold
-__device__ __forceinline__ bool calculate_populations(Ctl &C, const LvgDevProblem &P, const LvgModeLines &M, Slot &S, Smem &sm,
-                                      const LvgLaunch &Lc, int max_nb, int accel) {
+__device__ __forceinline__ bool calculate_populations(Ctl &C, const LvgDevProblem &P, const LvgModeLines &M,
+                                                      Slot &S, Smem &sm, const LvgLaunch &Lc, int max_nb, int accel) {
     const int N = P.N;
     C.acceleration = accel;
     C.accel_start = Lc.accel_start;
@@ -754,13 +785,15 @@ __device__ __forceinline__ Slot make_slot(const LvgDevProblem &P, const LvgLaunc
 __device__ __forceinline__ void solve_layer(const LvgDevProblem &P, const LvgLaunch &Lc, int l, Slot &S, Smem &sm) {
     const int N = P.N, t = threadIdx.x;
     const LvgModeLines &M = Lc.line_overlap ? P.overlap : P.plain;
+    TSTAMP(ts0);
     layer_setup(P, Lc, l, sm);
     double *pops = Lc.pops + (int64_t)l * N;
     lvg_layer_status *st = reinterpret_cast<lvg_layer_status *>(Lc.status) + l;
     const bool need_boundary = (Lc.init != LVG_INIT_GIVEN);
     build_collision_operators(P, sm, S.K, need_boundary ? S.A : nullptr);
+    TACC(PH_SETUP, ts0);
 
-    // initial guess
+    // initial guess (radiative_transfer.cpp:247-252)
     bool from_prev = false;
     if (Lc.init == LVG_INIT_WARM_CHAIN && Lc.chain && (Lc.lay_offset + l) > 0) {
         const lvg_layer_status *ps = reinterpret_cast<const lvg_layer_status *>(Lc.status) + l - 1;
@@ -773,7 +806,9 @@ __device__ __forceinline__ void solve_layer(const LvgDevProblem &P, const LvgLau
         for (int i = t; i < N; i += BT) { sm.pold[i] = pops[i - N]; S.given[i] = pops[i - N]; }
         __syncthreads();
     } else {
+        TSTAMP(tb0);
         boundary_layer_populations(P, S, sm);
+        TACC(PH_BOUNDARY, tb0);
         for (int i = t; i < N; i += BT) S.given[i] = sm.pold[i];
         __syncthreads();
     }
@@ -785,6 +820,7 @@ __device__ __forceinline__ void solve_layer(const LvgDevProblem &P, const LvgLau
     const int accel = Lc.acceleration;
     bool found = calculate_populations(C, P, M, S, sm, Lc, accel ? Lc.max_iter_acc : Lc.max_iter_plain, accel);
     int iters = C.iter_nb, retry = 0;
+    // retry without acceleration (radiative_transfer.cpp:258-276)
     if (!found && accel && Lc.allow_plain_retry) {
         for (int i = t; i < N; i += BT) sm.pold[i] = S.given[i];
         __syncthreads();
@@ -863,3 +899,14 @@ extern "C" int lvg_kernel_block_threads(void) { return lvg::BT; }
 extern "C" hipError_t lvg_kernel_occupancy(int *blocks_per_cu) {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, lvg::solve_kernel, lvg::BT, 0);
 }
+
+#ifdef LVG_PHASE_TIMERS
+extern "C" int lvg_debug_phase_cycles(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lvg::lvg_phase_cycles), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(lvg::lvg_phase_cycles), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

@@ -14,7 +14,7 @@ import numpy as np
 from . import abi
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "_lib", "liblvg_amd.so")
+LIB_PATH = os.environ.get("LVG_LIB_PATH") or os.path.join(_PKG, "_lib", "liblvg_amd.so")
 
 # every symbol include/lvg_amd.h declares
 EXPORTS = ("lvg_abi_version", "lvg_solve_opts_default", "lvg_create", "lvg_destroy", "lvg_last_error",
