@@ -55,16 +55,22 @@ constexpr double MIN_COLLISION_RATE    = 1.e-99;
 constexpr double INV_TRANS_FACTOR      = -0.1;
 constexpr double MIN_LINE_OPACITY      = 1.e-99;
 
+constexpr int TC = 4;                 // columns per thread in the LU register tile (8 rows x TC)
+constexpr int WB = 8 * TC;            // LU block-column width
+
 struct Smem {
-    double pold[NMAX], pnew[NMAX], bvec[NMAX];
-    double red[64];
-    int    ired[64];
-    int    piv[NB];
+    double pold[NMAX], pnew[NMAX], bvec[NMAX], blog[NMAX];
+    int    perm[NMAX];          // LU row permutation: logical position -> physical row
+    int    pos[NMAX];           // its inverse: physical row -> logical position
+    double red[8];
+    int    ired[8];
+    double pv[2][NB + 2];       // panel pivot-row broadcast, double buffered
+    int    pvi[2][2];
     double L11[NB][NB + 1];
-    double LT[NB][NMAX + 4];
+    double Ub[NB][WB + 2];      // U rows of one chunk across the block column
     union {
-        double P[NMAX][NB + 1];
-        double U[NB][NMAX + 4];
+        double P[NMAX][NB + 1]; // panel, physical rows
+        double LT[NB][NMAX];    // L of one chunk, transposed, physical rows
     } pu;
     // per-layer scalars
     double T, Te, vw, vgrad, nmol, ne;
@@ -83,6 +89,48 @@ __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
     return v;
+}
+
+// ---- DPP wave reductions (gfx9 row_shr / row_bcast sequence; the result lands in
+//      lane 63 and is broadcast with readlane). old == src makes lanes without a
+//      DPP source keep their own value, the identity of max/min.
+template <int CTRL, int ROW, int BANK>
+__device__ __forceinline__ double dpp_d(double x) {
+    int lo = __double2loint(x), hi = __double2hiint(x);
+    lo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROW, BANK, false);
+    hi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROW, BANK, false);
+    return __hiloint2double(hi, lo);
+}
+template <int CTRL, int ROW, int BANK>
+__device__ __forceinline__ int dpp_i(int x) {
+    return __builtin_amdgcn_update_dpp(x, x, CTRL, ROW, BANK, false);
+}
+__device__ __forceinline__ double wave_max_dpp(double v) {
+    v = fmax(v, dpp_d<0x111, 0xf, 0xf>(v));   // row_shr:1
+    v = fmax(v, dpp_d<0x112, 0xf, 0xf>(v));   // row_shr:2
+    v = fmax(v, dpp_d<0x113, 0xf, 0xf>(v));   // row_shr:3
+    v = fmax(v, dpp_d<0x114, 0xf, 0xe>(v));   // row_shr:4
+    v = fmax(v, dpp_d<0x118, 0xf, 0xc>(v));   // row_shr:8
+    v = fmax(v, dpp_d<0x142, 0xa, 0xf>(v));   // row_bcast:15
+    v = fmax(v, dpp_d<0x143, 0xc, 0xf>(v));   // row_bcast:31
+    int lo = __builtin_amdgcn_readlane(__double2loint(v), 63);
+    int hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ int wave_min_dpp(int v) {
+    v = min(v, dpp_i<0x111, 0xf, 0xf>(v));
+    v = min(v, dpp_i<0x112, 0xf, 0xf>(v));
+    v = min(v, dpp_i<0x113, 0xf, 0xf>(v));
+    v = min(v, dpp_i<0x114, 0xf, 0xe>(v));
+    v = min(v, dpp_i<0x118, 0xf, 0xc>(v));
+    v = min(v, dpp_i<0x142, 0xa, 0xf>(v));
+    v = min(v, dpp_i<0x143, 0xc, 0xf>(v));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ double readlane_d(double x, int lane) {
+    int lo = __builtin_amdgcn_readlane(__double2loint(x), lane);
+    int hi = __builtin_amdgcn_readlane(__double2hiint(x), lane);
+    return __hiloint2double(hi, lo);
 }
 
 __device__ __forceinline__ double block_max(double v, Smem &sm) {
@@ -423,166 +471,272 @@ __device__ __forceinline__ double assemble_and_residual(const LvgDevProblem &P, 
         A[d * N + d] = (d == 0) ? 1. : a;
     }
     __syncthreads();
-    double emax = 0.;
-    for (int i = t; i < N; i += BT) {
-        double s = (i == 0) ? 1. : 0.;
-        const double *row = A + (int64_t)i * N;
-        for (int j = 0; j < N; j++) s = s - row[j] * pop[j];
-        df[i] = s;
-        emax = fmax(emax, fabs(s));
+    // residual through LDS in 16-column chunks: global reads coalesced along rows,
+    // each thread still sums its own row in ascending j (bit-exact with the oracle)
+    double s_acc = (t == 0) ? 1. : 0.;
+    for (int c0 = 0; c0 < N; c0 += NB) {
+        const int nc = min(NB, N - c0);
+        for (int e = t; e < N * NB; e += BT) {
+            int r = e / NB, c = e - r * NB;
+            if (c < nc) sm.pu.P[r][c] = A[(int64_t)r * N + c0 + c];
+        }
+        __syncthreads();
+        if (t < N)
+            for (int c = 0; c < nc; c++) s_acc = s_acc - sm.pu.P[t][c] * pop[c0 + c];
+        __syncthreads();
     }
+    double emax = 0.;
+    if (t < N) { df[t] = s_acc; emax = fabs(s_acc); }
     return block_max(emax, sm);
 }
 
 // ------------------------------------------------------------------------------
-// blocked right-looking LU with partial pivoting, b solved alongside.
-// A: N x N row-major (lda = N) in the slot workspace; b: LDS [N]; on return b = x.
-// Every element receives fma(-l_ik, u_kj, a_ij) for k ascending, exactly the
-// sequence of the unblocked oracle (oracle_lu_solve).
+// Left-looking blocked LU with partial pivoting, b eliminated alongside.
+//
+// A: N x N row-major (physical rows) in the slot workspace, read once per block
+// column and overwritten in place by the factors (L below the pivots, U in the
+// pivot rows), never row-swapped: pivoting is virtual (perm/pos in LDS).
+// Block columns of WB = 64 columns live in registers, an 8x8 fp64 tile per thread
+// (rows 8*rg.., cols 8*cg..). For each 16-wide chunk kk to the left (earlier block
+// columns, then the block's own chunks once factored): the chunk's pivot rows are
+// solved against L11 (TRSM -> U rows, stored to A), then every row below is updated
+// with the chunk's L (staged transposed in LDS) and those U rows. Chunks are
+// factored by all four waves, one row per thread in registers (see below).
+//
+// Every element receives fma(-l_ik, u_kj, a_ij) for k ascending and the pivots are
+// chosen from identical values, so the result equals the unblocked, physically
+// pivoting oracle (oracle_lu_solve) bit for bit. On return sm.blog holds x.
+// b: LDS [N] indexed by physical row.
 // ------------------------------------------------------------------------------
+__device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, double *b, Smem &sm) {
+    // chunk columns kk..kk+nb-1 are in sm.pu.P[p][0..nb) for every physical row p;
+    // rows with pos[p] >= kk take part. One row per thread (N <= NMAX = BT).
+    const int t = threadIdx.x, w = t >> 6;
+    double rw[NB];
+    const bool valid = t < N;
+    const int p = valid ? t : 0;
+    bool act = valid && sm.pos[p] >= kk;
+    int lp = act ? sm.pos[p] - kk : 0x7fffffff;
+#pragma unroll
+    for (int j = 0; j < NB; j++) rw[j] = sm.pu.P[p][j];
+#pragma clang loop unroll(full)
+    for (int c = 0; c < NB; c++) {
+        if (c < nb) {
+            const int buf = c & 1;
+            const double v = act ? fabs(rw[c]) : -1.;
+            const double wmax = wave_max_dpp(v);
+            const int wmin = wave_min_dpp((v == wmax && act) ? lp : 0x7fffffff);
+            if ((t & 63) == 0) { sm.red[4 * buf + w] = wmax; sm.ired[4 * buf + w] = wmin; }
+            __syncthreads();
+            double vmax = sm.red[4 * buf];
+            int lmin = sm.ired[4 * buf];
+#pragma unroll
+            for (int i = 1; i < NW; i++) {
+                const double ov = sm.red[4 * buf + i];
+                const int oi = sm.ired[4 * buf + i];
+                if (ov > vmax || (ov == vmax && oi < lmin)) { vmax = ov; lmin = oi; }
+            }
+            const bool owner = act && lp == lmin;
+            if (owner) {
+#pragma unroll
+                for (int j = 0; j < NB; j++) if (j >= c) sm.pv[buf][j] = rw[j];
+                sm.pvi[buf][0] = p;
+            }
+            __syncthreads();
+            const double piv = sm.pv[buf][c];
+            const double bc = b[sm.pvi[buf][0]];
+            if (owner) { act = false; lp = c; }
+            else if (lp == c) lp = lmin;
+            if (act) {
+                const double l = rw[c] / piv;
+                rw[c] = l;
+#pragma unroll
+                for (int j = 0; j < NB; j++) if (j > c) rw[j] = fma(-l, sm.pv[buf][j], rw[j]);
+                b[p] = fma(-l, bc, b[p]);
+            }
+        }
+    }
+    __syncthreads();
+    if (valid && sm.pos[p] >= kk) {
+        // rows of this chunk and below: factors back to A (physical row p)
+#pragma unroll
+        for (int j = 0; j < NB; j++) if (j < nb) A[(int64_t)p * N + kk + j] = rw[j];
+        sm.perm[kk + lp] = p;
+        sm.pos[p] = kk + lp;
+#pragma unroll
+        for (int j = 0; j < NB; j++) sm.pu.P[p][j] = rw[j];
+    }
+    __syncthreads();
+}
+
 __device__ __forceinline__ void block_lu_solve(double *A, int N, double *b, Smem &sm) {
     const int t = threadIdx.x;
-    for (int k0 = 0; k0 < N; k0 += NB) {
+    const int rg = t >> 3, cg = t & 7;
+    for (int i = t; i < N; i += BT) { sm.perm[i] = i; sm.pos[i] = i; }
+    __syncthreads();
+    for (int c0 = 0; c0 < N; c0 += WB) {
         TSTAMP(tp0);
-        const int nb = min(NB, N - k0);
-        const int R = N - k0;
-        // ---- panel load (rows k0..N-1, cols k0..k0+nb-1)
-        for (int e = t; e < R * nb; e += BT) {
-            int r = e / nb, c = e - r * nb;
-            sm.pu.P[r][c] = A[(int64_t)(k0 + r) * N + k0 + c];
-        }
-        __syncthreads();
-        // ---- panel factorization
-        for (int c = 0; c < nb; c++) {
-            double v = -1.;
-            int idx = 0x7fffffff;
-            for (int r = c + t; r < R; r += BT) {
-                double a = fabs(sm.pu.P[r][c]);
-                if (a > v) { v = a; idx = r; }
+        const int wJ = min(WB, N - c0);
+        double acc[8][TC];
+        // ---- block column c0..c0+wJ-1 into registers (physical rows, coalesced)
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+            for (int j = 0; j < TC; j++) {
+                const int pr = 8 * rg + i, col = TC * cg + j;
+                acc[i][j] = (pr < N && col < wJ) ? A[(int64_t)pr * N + c0 + col] : 0.;
             }
-            int p = block_argmax(v, idx, sm);
-            if (p != c) {
-                for (int j = t; j < nb; j += BT) {
-                    double x = sm.pu.P[c][j]; sm.pu.P[c][j] = sm.pu.P[p][j]; sm.pu.P[p][j] = x;
-                }
-                if (t == 0) { double x = b[k0 + c]; b[k0 + c] = b[k0 + p]; b[k0 + p] = x; }
-            }
-            if (t == 0) sm.piv[c] = p;
-            __syncthreads();
-            const double piv = sm.pu.P[c][c];
-            const double bc = b[k0 + c];
-            for (int r = c + 1 + t; r < R; r += BT) {
-                double lr = sm.pu.P[r][c] / piv;
-                sm.pu.P[r][c] = lr;
-                for (int j = c + 1; j < nb; j++) sm.pu.P[r][j] = fma(-lr, sm.pu.P[c][j], sm.pu.P[r][j]);
-                b[k0 + r] = fma(-lr, bc, b[k0 + r]);
-            }
-            __syncthreads();
-        }
-        // ---- keep U11 in A (for back substitution), L11 and L21^T in LDS
-        for (int e = t; e < nb * nb; e += BT) {
-            int r = e / nb, c = e - r * nb;
-            double x = sm.pu.P[r][c];
-            if (c >= r) A[(int64_t)(k0 + r) * N + k0 + c] = x;
-            sm.L11[r][c] = (c < r) ? x : 0.;
-        }
-        for (int e = t; e < (R - nb) * nb; e += BT) {
-            int c = e / (R - nb), r = e - c * (R - nb);
-            sm.LT[c][r] = sm.pu.P[nb + r][c];
-        }
-        __syncthreads();
-        TACC(PH_PANEL, tp0);
-        TSTAMP(tp1);
-        const int C2 = N - k0 - nb;
-        if (C2 > 0) {
-            // ---- row interchanges + TRSM on trailing columns (thread per column),
-            //      U12 = L11^-1 A12 formed in place in LDS
-            for (int jj = t; jj < C2; jj += BT) {
-                const int j = k0 + nb + jj;
-                for (int c = 0; c < nb; c++) {
-                    int p = sm.piv[c];
-                    if (p != c) {
-                        double x = A[(int64_t)(k0 + c) * N + j];
-                        A[(int64_t)(k0 + c) * N + j] = A[(int64_t)(k0 + p) * N + j];
-                        A[(int64_t)(k0 + p) * N + j] = x;
+        TACC(PH_GEMM, tp0);
+        for (int kk = 0; kk < c0 + wJ; kk += NB) {
+            const int nb = min(NB, N - kk);
+            int jlo;                                   // first block-local column to update
+            if (kk >= c0) {
+                // ---- a chunk of this block column: all updates from k < kk are in; factor it
+                TSTAMP(tp1);
+                const int g = cg - (kk - c0) / TC;     // this thread's column group within the chunk
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const int pr = 8 * rg + i;
+                    if (pr < N && g >= 0 && g < NB / TC) {
+#pragma unroll
+                        for (int j = 0; j < TC; j++) sm.pu.P[pr][TC * g + j] = acc[i][j];
                     }
                 }
-                for (int i = 0; i < nb; i++) {
-                    double s = A[(int64_t)(k0 + i) * N + j];
-                    for (int m = 0; m < i; m++) s = fma(-sm.L11[i][m], sm.pu.U[m][jj], s);
-                    sm.pu.U[i][jj] = s;
-                    A[(int64_t)(k0 + i) * N + j] = s;
+                __syncthreads();
+                panel_factor(A, N, kk, nb, b, sm);
+                for (int e = t; e < NB * NB; e += BT) {
+                    const int r = e / NB, m = e - r * NB;
+                    sm.L11[r][m] = (r < nb && m < r) ? sm.pu.P[sm.perm[kk + r]][m] : 0.;
                 }
+                __syncthreads();
+                TACC(PH_PANEL, tp1);
+                jlo = kk - c0 + nb;
+                if (jlo >= wJ) break;                  // last chunk of the block column
+            } else {
+                for (int e = t; e < NB * NB; e += BT) {
+                    const int r = e / NB, m = e - r * NB;
+                    sm.L11[r][m] = (r < nb && m < r) ? A[(int64_t)sm.perm[kk + r] * N + kk + m] : 0.;
+                }
+                jlo = 0;
             }
-            __syncthreads();
-            TACC(PH_TRSM, tp1);
             TSTAMP(tp2);
-            // ---- trailing update A22 -= L21 * U12, 4x4 register tiles, 64x64 per pass
-            const int R2 = R - nb;
-            const int tr = t >> 4, tc = t & 15;
-            const int ntr = (R2 + 63) >> 6, ntc = (C2 + 63) >> 6;
-            for (int tile = 0; tile < ntr * ntc; tile++) {
-                const int ti = tile / ntc, tj = tile - ti * ntc;
-                const int r0 = ti * 64 + tr * 4, c0 = tj * 64 + tc * 4;
-                double acc[4][4];
+            // ---- pivot rows of chunk kk (logical kk..kk+nb-1): their current values
+            //      in this block column -> Ub (owners write from registers)
 #pragma unroll
-                for (int i = 0; i < 4; i++)
+            for (int i = 0; i < 8; i++) {
+                const int pr = 8 * rg + i;
+                if (pr < N) {
+                    const int q = sm.pos[pr] - kk;
+                    if (q >= 0 && q < nb) {
 #pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        int r = r0 + i, cc = c0 + j;
-                        acc[i][j] = (r < R2 && cc < C2) ? A[(int64_t)(k0 + nb + r) * N + k0 + nb + cc] : 0.;
+                        for (int j = 0; j < TC; j++) sm.Ub[q][TC * cg + j] = acc[i][j];
                     }
-                for (int c = 0; c < nb; c++) {
-                    double a[4], bb[4];
-#pragma unroll
-                    for (int i = 0; i < 4; i++) a[i] = sm.LT[c][min(r0 + i, NMAX - 1)];
-#pragma unroll
-                    for (int j = 0; j < 4; j++) bb[j] = sm.pu.U[c][min(c0 + j, NMAX - 1)];
-#pragma unroll
-                    for (int i = 0; i < 4; i++)
-#pragma unroll
-                        for (int j = 0; j < 4; j++) acc[i][j] = fma(-a[i], bb[j], acc[i][j]);
                 }
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        int r = r0 + i, cc = c0 + j;
-                        if (r < R2 && cc < C2) A[(int64_t)(k0 + nb + r) * N + k0 + nb + cc] = acc[i][j];
-                    }
             }
             __syncthreads();
-            TACC(PH_GEMM, tp2);
+            // ---- TRSM U = L11^-1 Ub: wave w owns columns [WB/4*w, WB/4*(w+1)), lane l row
+            //      l&15 of TC/2 of them; x_r takes its updates for m ascending (oracle
+            //      order), x_m broadcast by lane shuffle. U rows to A for back substitution.
+            {
+                const int l = t & 63, w = t >> 6, r = l & 15;
+                double x[TC / 2];
+#pragma unroll
+                for (int q = 0; q < TC / 2; q++) {
+                    const int c = (WB / 4) * w + (l >> 4) + 4 * q;
+                    x[q] = (r < nb && c < wJ) ? sm.Ub[r][c] : 0.;
+                }
+                for (int m = 0; m < nb - 1; m++) {
+                    const double lm = sm.L11[r][m];
+#pragma unroll
+                    for (int q = 0; q < TC / 2; q++) {
+                        const double y = __shfl(x[q], (l & ~15) + m, 64);
+                        if (r > m) x[q] = fma(-lm, y, x[q]);
+                    }
+                }
+                if (r < nb) {
+                    const int64_t prow = (int64_t)sm.perm[kk + r] * N + c0;
+#pragma unroll
+                    for (int q = 0; q < TC / 2; q++) {
+                        const int c = (WB / 4) * w + (l >> 4) + 4 * q;
+                        if (c >= jlo && c < wJ) { sm.Ub[r][c] = x[q]; A[prow + c] = x[q]; }
+                    }
+                }
+            }
+            // ---- L of chunk kk for the rows below it, transposed into LDS (thread per row)
+            {
+                const int pr = t;
+                const bool lact = pr < N && sm.pos[pr] >= kk + nb;
+                const double *src = A + (int64_t)(lact ? pr : 0) * N + kk;
+#pragma unroll
+                for (int m = 0; m < NB; m++) sm.pu.LT[m][pr] = (lact && m < nb) ? src[m] : 0.;
+            }
+            __syncthreads();
+            TACC(PH_TRSM, tp2);
+            TSTAMP(tp3);
+            // ---- rank-nb update of the rows below (8x8 register tiles)
+            bool ract[8];
+            bool any = false;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int pr = 8 * rg + i;
+                ract[i] = pr < N && sm.pos[pr] >= kk + nb;
+                any = any || ract[i];
+            }
+            if (any && TC * cg + TC - 1 >= jlo) {
+                for (int m = 0; m < nb; m++) {
+                    double a[8], u[TC];
+#pragma unroll
+                    for (int i = 0; i < 8; i++) a[i] = sm.pu.LT[m][8 * rg + i];
+#pragma unroll
+                    for (int j = 0; j < TC; j++) u[j] = sm.Ub[m][TC * cg + j];
+#pragma unroll
+                    for (int i = 0; i < 8; i++)
+#pragma unroll
+                        for (int j = 0; j < TC; j++) {
+                            const double r = fma(-a[i], u[j], acc[i][j]);
+                            acc[i][j] = (ract[i] && TC * cg + j >= jlo) ? r : acc[i][j];
+                        }
+                }
+            }
+            __syncthreads();
+            TACC(PH_GEMM, tp3);
         }
-        __syncthreads();
     }
     TSTAMP(tb0);
-    // ---- back substitution U x = y, blocked by NB from the bottom: wave 0 solves
-    //      the diagonal block through LDS, then all threads update the rows above;
-    //      every b[i] receives its updates for k descending, as in the oracle
+    // ---- back substitution U x = y in logical order, blocked by NB from the bottom:
+    //      wave 0 solves the diagonal block through LDS, then all threads update the
+    //      rows above; every entry receives its updates for k descending (oracle order)
+    for (int i = t; i < N; i += BT) sm.blog[i] = b[sm.perm[i]];
+    __syncthreads();
     const int nblk = (N + NB - 1) / NB;
     for (int kb = nblk - 1; kb >= 0; kb--) {
         const int k0 = kb * NB, nb = min(NB, N - k0);
         for (int e = t; e < nb * nb; e += BT) {
             int r = e / nb, c = e - r * nb;
-            sm.L11[r][c] = A[(int64_t)(k0 + r) * N + k0 + c];
+            sm.L11[r][c] = A[(int64_t)sm.perm[k0 + r] * N + k0 + c];
         }
         __syncthreads();
         if (t < 64) {
             for (int m = nb - 1; m >= 0; m--) {
-                const double xm = b[k0 + m] / sm.L11[m][m];
+                const double xm = sm.blog[k0 + m] / sm.L11[m][m];
                 __builtin_amdgcn_wave_barrier();
-                if (t < m) b[k0 + t] = fma(-sm.L11[t][m], xm, b[k0 + t]);
-                else if (t == m) b[k0 + m] = xm;
+                if (t < m) sm.blog[k0 + t] = fma(-sm.L11[t][m], xm, sm.blog[k0 + t]);
+                else if (t == m) sm.blog[k0 + m] = xm;
+                __builtin_amdgcn_s_waitcnt(0xc07f);
                 __builtin_amdgcn_wave_barrier();
             }
         }
         __syncthreads();
         for (int i = t; i < k0; i += BT) {
-            double s = b[i];
-            const double *row = A + (int64_t)i * N + k0;
-            for (int m = nb - 1; m >= 0; m--) s = fma(-row[m], b[k0 + m], s);
-            b[i] = s;
+            const double *row = A + (int64_t)sm.perm[i] * N + k0;
+            double u[NB];
+#pragma unroll
+            for (int m = 0; m < NB; m++) u[m] = (m < nb) ? row[m] : 0.;
+            double s = sm.blog[i];
+#pragma unroll
+            for (int m = NB - 1; m >= 0; m--)
+                if (m < nb) s = fma(-u[m], sm.blog[k0 + m], s);
+            sm.blog[i] = s;
         }
         __syncthreads();
     }
@@ -620,7 +774,7 @@ __device__ __forceinline__ double calc_new_pop(const LvgDevProblem &P, const Lvg
     for (int i = t; i < N; i += BT) sm.bvec[i] = (i == 0) ? 1. : 0.;
     __syncthreads();
     block_lu_solve(S.A, N, sm.bvec, sm);
-    for (int i = t; i < N; i += BT) sm.pnew[i] = sm.bvec[i];
+    for (int i = t; i < N; i += BT) sm.pnew[i] = sm.blog[i];
     __syncthreads();
     return eq;
 }
@@ -762,7 +916,7 @@ __device__ __forceinline__ void boundary_layer_populations(const LvgDevProblem &
     for (int i = t; i < N; i += BT) sm.bvec[i] = (i == 0) ? 1. : 0.;
     __syncthreads();
     block_lu_solve(S.A, N, sm.bvec, sm);   // S.A holds the boundary matrix
-    for (int i = t; i < N; i += BT) sm.pold[i] = sm.bvec[i];
+    for (int i = t; i < N; i += BT) sm.pold[i] = sm.blog[i];
     __syncthreads();
 }
 
@@ -877,7 +1031,7 @@ __global__ void __launch_bounds__(BT, 2) debug_kernel(const LvgDevProblem *__res
     for (int i = t; i < N; i += BT) { Lc.dbg_df[i] = S.df[i]; sm.bvec[i] = (i == 0) ? 1. : 0.; }
     __syncthreads();
     block_lu_solve(S.A, N, sm.bvec, sm);
-    for (int i = t; i < N; i += BT) Lc.pops[i] = sm.bvec[i];
+    for (int i = t; i < N; i += BT) Lc.pops[i] = sm.blog[i];
     if (t == 0) Lc.dbg_df[N] = eq;
 }
 
