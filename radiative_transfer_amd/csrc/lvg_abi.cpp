@@ -38,7 +38,7 @@ struct DevBuf {
 };
 
 struct ModeHost {
-    std::vector<int> u, l, unit0, unit1, dptr, dent, cptr, cr, cy;
+    std::vector<int> u, l, unit0, unit1, dptr, dent, cptr, cr, cy, li;
     std::vector<double> aul, alu, e, sigma;
     int interleaved = 1;
 };
@@ -290,6 +290,11 @@ void finish_mode(ModeHost &m, const lvg_problem *prob) {
     }
     m.dptr[N] = (int)m.dent.size();
     m.cptr[N] = (int)m.cr.size();
+    // dense map for the fused assembly: li[r*N + d] = y index of the line joining
+    // levels r and d (its term lands at row r of column d), -1 if none
+    m.li.assign((size_t)N * N, -1);
+    for (int d = 0; d < N; d++)
+        for (int e = m.cptr[d]; e < m.cptr[d + 1]; e++) m.li[(size_t)m.cr[e] * N + d] = m.cy[e];
 }
 
 // hfs_lines::sort / split (iteration_lvg.cpp:259-302), stale minimum kept (quirk q6)
@@ -373,6 +378,7 @@ int upload_mode(lvg_handle *h, const ModeHost &m, LvgModeLines &d) {
     if ((rc = upload(h, m.cptr.data(), m.cptr.size(), &d.col_ptr))) return rc;
     if ((rc = upload(h, m.cr.data(), m.cr.size(), &d.col_r))) return rc;
     if ((rc = upload(h, m.cy.data(), m.cy.size(), &d.col_y))) return rc;
+    if ((rc = upload(h, m.li.data(), m.li.size(), &d.line_idx))) return rc;
     d.diag_interleaved = m.interleaved;
     return LVG_OK;
 }

@@ -44,6 +44,7 @@ struct LvgModeLines {          // one radiative scheme (plain LVG or line overla
     const int    *col_ptr;     // [N+1]
     const int    *col_r;
     const int    *col_y;
+    const int    *line_idx;    // [N*N] y index of the term at (row r, column d), -1 if none
     // diagonal order: interleaved with the collision terms (plain scheme,
     // iteration_lvg.cpp:118-147) or after all of them in line order (overlap
     // scheme, iteration_lvg.cpp:354-412)

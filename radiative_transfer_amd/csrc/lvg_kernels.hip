@@ -60,6 +60,7 @@ constexpr int WB = 8 * TC;            // LU block-column width
 
 struct Smem {
     double pold[NMAX], pnew[NMAX], bvec[NMAX], blog[NMAX];
+    double diag[NMAX];          // assembled diagonal of the rate matrix (fused assembly)
     int    perm[NMAX];          // LU row permutation: logical position -> physical row
     int    pos[NMAX];           // its inverse: physical row -> logical position
     double red[8];
@@ -77,6 +78,12 @@ struct Smem {
     double cc[LVG_MAX_COMBOS];
     double teff[LVG_MAX_TABLES];
     int    lo[LVG_MAX_TABLES];
+    const double *tcol[LVG_MAX_TABLES];   // coefficients at T index lo (T-major row)
+    int64_t timax[LVG_MAX_TABLES];        // pairs per T row
+    double tdt[LVG_MAX_TABLES];           // tgrid[lo+1] - tgrid[lo]
+    double tx[LVG_MAX_TABLES];            // min(T, tmax) - tgrid[lo]
+    int8_t ttab[LVG_MAX_CLASSES][LVG_MAX_TERMS], tcombo[LVG_MAX_CLASSES][LVG_MAX_TERMS];
+    int8_t tet[LVG_MAX_CLASSES], tgrp[LVG_MAX_CLASSES];
     double dust[LVG_MAX_DUST];
     double hist_acc[32];
     int    layer;
@@ -276,72 +283,97 @@ __device__ __forceinline__ void layer_setup(const LvgDevProblem &P, const LvgLau
             sm.lo[tb] = lo;
             double tmax = tg[jm - 1];
             sm.teff[tb] = temp < tmax ? temp : tmax;
+            const int64_t imax = (int64_t)P.tab_nb_lev[tb] * (P.tab_nb_lev[tb] - 1) / 2;
+            sm.timax[tb] = imax;
+            sm.tcol[tb] = P.tab_coeff + P.tab_c_off[tb] + (int64_t)lo * imax;
+            sm.tdt[tb] = tg[lo + 1] - tg[lo];
+            sm.tx[tb] = sm.teff[tb] - tg[lo];
         }
     }
     __syncthreads();
 }
 
-// collision_data::get_rate (coll_rates.cpp:54-69), T-major table
-__device__ __forceinline__ double table_rate(const LvgDevProblem &P, const Smem &sm, int tb, int pair) {
-    const int lo = sm.lo[tb];
-    const int64_t imax = (int64_t)P.tab_nb_lev[tb] * (P.tab_nb_lev[tb] - 1) / 2;
-    const double *c = P.tab_coeff + P.tab_c_off[tb];
-    const double *tg = P.tab_tgrid + P.tab_tg_off[tb];
-    double c0 = c[(int64_t)lo * imax + pair], c1 = c[(int64_t)(lo + 1) * imax + pair];
-    double deriv = (c1 - c0) / (tg[lo + 1] - tg[lo]);
-    return c0 + deriv * (sm.teff[tb] - tg[lo]);
+// collision_data::get_rate (coll_rates.cpp:54-69), T-major table; the per-layer
+// interval data (row pointer, dT, T - tgrid[lo]) sit in LDS (layer_setup)
+__device__ __forceinline__ double table_rate(const Smem &sm, int tb, int pair) {
+    const double *c = sm.tcol[tb];
+    const double c0 = c[pair], c1 = c[sm.timax[tb] + pair];
+    const double deriv = (c1 - c0) / sm.tdt[tb];
+    return c0 + deriv * sm.tx[tb];
+}
+
+// the compiled molecule rule, copied to LDS once per launch
+__device__ __forceinline__ void load_rule_table(const LvgDevProblem &P, Smem &sm) {
+    for (int e = threadIdx.x; e < LVG_MAX_CLASSES * LVG_MAX_TERMS; e += BT) {
+        (&sm.ttab[0][0])[e] = (&P.terms.table[0][0])[e];
+        (&sm.tcombo[0][0])[e] = (&P.terms.combo[0][0])[e];
+    }
+    for (int e = threadIdx.x; e < LVG_MAX_CLASSES; e += BT) {
+        sm.tet[e] = P.terms.etable[e];
+        sm.tgrp[e] = P.terms.group[e];
+    }
+    __syncthreads();
 }
 
 // Collision operator K (neutral + electron rates; iteration_lvg.cpp:121-131) and
 // the boundary-layer matrix B (neutrals + A/2; iteration_control.cpp:69-85),
 // row-major M[final][initial]. K keeps off-diagonals only (its diagonal is
 // rebuilt every iteration in the reference's order); B gets its diagonal as the
-// ascending column sum, row 0 <- 1.
+// ascending column sum, row 0 <- 1. Level pairs (f > s) are walked in 16x16 tiles
+// of the lower triangle, one pair per thread: table reads and the K[f][s] writes
+// are 128-byte row segments, every lane is busy.
 __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P, Smem &sm, double *K, double *B) {
     const int N = P.N, t = threadIdx.x;
     const double T = sm.T, Te = sm.Te;
-    for (int f = 1; f < N; f++) {
-        const int base = f * (f - 1) / 2;
-        for (int s = t; s < f; s += BT) {
-            const int pair = base + s;
-            const int cls = P.pair_class[pair];
-            const int grp = P.terms.group[cls];
-            double dn = 0., gsum = 0.;
-            int ng = 0;
+    const int nt = (N + 15) >> 4, ntiles = nt * (nt + 1) / 2;
+    const int fl = t >> 4, sl = t & 15;
+    int F = 0, S = 0;
+#pragma unroll 2
+    for (int q = 0; q < ntiles; q++) {
+        const int f = 16 * F + fl, s = 16 * S + sl;
+        if (++S > F) { S = 0; F++; }
+        if (f >= N || s >= f) continue;
+        const int pair = f * (f - 1) / 2 + s;
+        const int cls = P.pair_class[pair];
+        const int grp = sm.tgrp[cls];
+        double dn = 0., gsum = 0.;
+        int ng = 0;
 #pragma unroll
-            for (int k = 0; k < LVG_MAX_TERMS; k++) {
-                int tb = P.terms.table[cls][k];
-                if (tb < 0) break;
-                double r = table_rate(P, sm, tb, pair) * sm.cc[P.terms.combo[cls][k]];
-                if (k < grp) dn = (k == 0) ? r : dn + r;
-                else { gsum = (ng == 0) ? r : gsum + r; ng++; }
-            }
-            if (ng) dn = dn + gsum;
-            const double de = P.energy[s] - P.energy[f];
-            double un = 0.;
-            if (dn > MIN_COLLISION_RATE) un = dn * lvg_exp(de * CM_INVERSE_TO_KELVINS / T) * P.g[f] / P.g[s];
-            else dn = 0.;
-            double dE = 0., uE = 0.;
-            int et = P.terms.etable[cls];
-            if (et >= 0) {
-                dE = table_rate(P, sm, et, pair) * sm.ne;
-                if (dE > MIN_COLLISION_RATE) uE = dE * lvg_exp(de * CM_INVERSE_TO_KELVINS / Te) * P.g[f] / P.g[s];
-                else dE = 0.;
-            }
-            K[s * N + f] = dn + dE;
-            K[f * N + s] = un + uE;
-            if (B) {
-                B[s * N + f] = 0.5 * P.einst[f * N + s] + dn;
-                B[f * N + s] = un;
-            }
+        for (int k = 0; k < LVG_MAX_TERMS; k++) {
+            const int tb = sm.ttab[cls][k];
+            if (tb < 0) break;
+            const double r = table_rate(sm, tb, pair) * sm.cc[sm.tcombo[cls][k]];
+            if (k < grp) dn = (k == 0) ? r : dn + r;
+            else { gsum = (ng == 0) ? r : gsum + r; ng++; }
+        }
+        if (ng) dn = dn + gsum;
+        const double de = P.energy[s] - P.energy[f];
+        double un = 0.;
+        if (dn > MIN_COLLISION_RATE) un = dn * lvg_exp(de * CM_INVERSE_TO_KELVINS / T) * P.g[f] / P.g[s];
+        else dn = 0.;
+        double dE = 0., uE = 0.;
+        const int et = sm.tet[cls];
+        if (et >= 0) {
+            dE = table_rate(sm, et, pair) * sm.ne;
+            if (dE > MIN_COLLISION_RATE) uE = dE * lvg_exp(de * CM_INVERSE_TO_KELVINS / Te) * P.g[f] / P.g[s];
+            else dE = 0.;
+        }
+        K[s * N + f] = dn + dE;
+        K[f * N + s] = un + uE;
+        if (B) {
+            B[s * N + f] = 0.5 * P.einst[f * N + s] + dn;
+            B[f * N + s] = un;
         }
     }
     __syncthreads();
     if (B) {
         for (int d = t; d < N; d += BT) {
             double a = 0.;
-            for (int r = 0; r < N; r++)
-                if (r != d) a = a - B[r * N + d];
+#pragma unroll 8
+            for (int r = 0; r < N; r++) {
+                const double v = B[r * N + d];
+                a = (r != d) ? a - v : a;
+            }
             B[d * N + d] = a;
         }
         __syncthreads();
@@ -438,57 +470,54 @@ __device__ __forceinline__ void compute_line_terms(const LvgDevProblem &P, const
     }
 }
 
-// A = K + radiative terms, row 0 <- 1 (iteration_lvg.cpp:117-151), as ONE pass
-// over the columns of K (thread d owns column d: coalesced row sweeps). The
-// diagonal is accumulated in the reference's order: for partner levels r
-// ascending, -rate(d->r) then, if a line joins d and r, -y (plain scheme); or
-// all collision terms first and the lines after, in line order (overlap scheme).
-// Then df = e0 - A n row by row in the reference's j order (:153-160).
-__device__ __forceinline__ double assemble_and_residual(const LvgDevProblem &P, const LvgModeLines &M,
-                                                        const double *K, double *A, const double *y,
-                                                        const double *pop, double *df, Smem &sm) {
+// Diagonal of the rate matrix (iteration_lvg.cpp:117-151): thread d folds column
+// d of K in the reference's order: for partner levels r ascending, -rate(d->r)
+// then, if a line joins d and r, -y (plain scheme); or all collision terms first
+// and the lines after, in line order (overlap scheme). The off-diagonal entries
+// are formed where the LU loads them (block_lu_solve<true>).
+__device__ __forceinline__ void column_diagonals(const LvgDevProblem &P, const LvgModeLines &M,
+                                                 const double *K, const double *y, Smem &sm) {
     const int N = P.N, t = threadIdx.x;
     for (int d = t; d < N; d += BT) {
         int e = M.col_ptr[d];
         const int e1 = M.col_ptr[d + 1];
         int nr = (e < e1) ? M.col_r[e] : N;
         double a = 0.;
-        for (int r = 0; r < N; r++) {
-            if (r == d) continue;
-            double v = K[r * N + d];
-            a = a - v;
-            if (r == nr) {
-                const double yy = y[M.col_y[e]];
-                if (M.diag_interleaved) a = a - yy;
-                v = v + yy;
-                e++;
-                nr = (e < e1) ? M.col_r[e] : N;
+        for (int r0 = 0; r0 < N; r0 += 8) {
+            double kv[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) kv[u] = (r0 + u < N) ? K[(r0 + u) * N + d] : 0.;
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int r = r0 + u;
+                if (r < N && r != d) {
+                    a = a - kv[u];
+                    if (r == nr) {
+                        if (M.diag_interleaved) a = a - y[M.col_y[e]];
+                        e++;
+                        nr = (e < e1) ? M.col_r[e] : N;
+                    }
+                }
             }
-            A[r * N + d] = (r == 0) ? 1. : v;
         }
         if (!M.diag_interleaved)
             for (int q = M.diag_ptr[d]; q < M.diag_ptr[d + 1]; q++) a = a - y[M.diag_ent[q]];
-        A[d * N + d] = (d == 0) ? 1. : a;
+        sm.diag[d] = a;
     }
     __syncthreads();
-    // residual through LDS in 16-column chunks: global reads coalesced along rows,
-    // each thread still sums its own row in ascending j (bit-exact with the oracle)
-    double s_acc = (t == 0) ? 1. : 0.;
-    for (int c0 = 0; c0 < N; c0 += NB) {
-        const int nc = min(NB, N - c0);
-        for (int e = t; e < N * NB; e += BT) {
-            int r = e / NB, c = e - r * NB;
-            if (c < nc) sm.pu.P[r][c] = A[(int64_t)r * N + c0 + c];
-        }
-        __syncthreads();
-        if (t < N)
-            for (int c = 0; c < nc; c++) s_acc = s_acc - sm.pu.P[t][c] * pop[c0 + c];
-        __syncthreads();
-    }
-    double emax = 0.;
-    if (t < N) { df[t] = s_acc; emax = fabs(s_acc); }
-    return block_max(emax, sm);
 }
+
+// Source of the matrix the LU factors: the assembled A already in the slot
+// (boundary layer), or fused: K + line terms + sm.diag, row 0 <- 1, formed while
+// each block column is loaded, with the residual df = e0 - A n accumulated on the
+// way (row by row in ascending column order, as iteration_lvg.cpp:153-160).
+struct LuSrc {
+    const double *K = nullptr, *y = nullptr;
+    const int *li = nullptr;
+    const double *pop = nullptr;   // LDS populations for the residual
+    double *df = nullptr;          // [N] residual out
+    double *dump = nullptr;        // optional [N*N] copy of the assembled matrix (debug)
+};
 
 // ------------------------------------------------------------------------------
 // Left-looking blocked LU with partial pivoting, b eliminated alongside.
@@ -569,9 +598,11 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
     __syncthreads();
 }
 
-__device__ __forceinline__ void block_lu_solve(double *A, int N, double *b, Smem &sm) {
+template <bool FUSED>
+__device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Smem &sm, const LuSrc &src = LuSrc()) {
     const int t = threadIdx.x;
     const int rg = t >> 3, cg = t & 7;
+    double s_acc = (t == 0) ? 1. : 0.;             // residual row t (FUSED)
     for (int i = t; i < N; i += BT) { sm.perm[i] = i; sm.pos[i] = i; }
     __syncthreads();
     for (int c0 = 0; c0 < N; c0 += WB) {
@@ -579,13 +610,54 @@ __device__ __forceinline__ void block_lu_solve(double *A, int N, double *b, Smem
         const int wJ = min(WB, N - c0);
         double acc[8][TC];
         // ---- block column c0..c0+wJ-1 into registers (physical rows, coalesced)
+        if (!FUSED) {
 #pragma unroll
-        for (int i = 0; i < 8; i++)
+            for (int i = 0; i < 8; i++)
 #pragma unroll
-            for (int j = 0; j < TC; j++) {
-                const int pr = 8 * rg + i, col = TC * cg + j;
-                acc[i][j] = (pr < N && col < wJ) ? A[(int64_t)pr * N + c0 + col] : 0.;
+                for (int j = 0; j < TC; j++) {
+                    const int pr = 8 * rg + i, col = TC * cg + j;
+                    acc[i][j] = (pr < N && col < wJ) ? A[(int64_t)pr * N + c0 + col] : 0.;
+                }
+        } else {
+            int li[8][TC];
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+#pragma unroll
+                for (int j = 0; j < TC; j++) {
+                    const int pr = 8 * rg + i, col = TC * cg + j;
+                    const bool ok = pr < N && col < wJ;
+                    const int64_t o = (int64_t)pr * N + c0 + col;
+                    acc[i][j] = ok ? src.K[o] : 0.;
+                    li[i][j] = ok ? src.li[o] : -1;
+                }
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+#pragma unroll
+                for (int j = 0; j < TC; j++) {
+                    const int pr = 8 * rg + i, d = c0 + TC * cg + j;
+                    double v = acc[i][j];
+                    if (li[i][j] >= 0) v = v + src.y[li[i][j]];
+                    if (pr == d) v = sm.diag[d < NMAX ? d : 0];
+                    if (pr == 0) v = 1.;
+                    acc[i][j] = v;
+                    if (src.dump && pr < N && TC * cg + j < wJ) src.dump[(int64_t)pr * N + d] = v;
+                }
+            // residual rows: 16 columns at a time through LDS, each thread its own row
+            for (int h = 0; h < wJ; h += NB) {
+                const int g = cg - h / TC;
+                if (g >= 0 && g < NB / TC) {
+#pragma unroll
+                    for (int i = 0; i < 8; i++)
+#pragma unroll
+                        for (int j = 0; j < TC; j++) sm.pu.P[8 * rg + i][TC * g + j] = acc[i][j];
+                }
+                __syncthreads();
+                const int nc = min(NB, wJ - h);
+                if (t < N)
+                    for (int c = 0; c < nc; c++) s_acc = s_acc - sm.pu.P[t][c] * src.pop[c0 + h + c];
+                __syncthreads();
             }
+        }
         TACC(PH_GEMM, tp0);
         for (int kk = 0; kk < c0 + wJ; kk += NB) {
             const int nb = min(NB, N - kk);
@@ -741,6 +813,9 @@ __device__ __forceinline__ void block_lu_solve(double *A, int N, double *b, Smem
         __syncthreads();
     }
     TACC(PH_BACKSUB, tb0);
+    double emax = 0.;
+    if (FUSED && t < N) { src.df[t] = s_acc; emax = fabs(s_acc); }
+    return FUSED ? block_max(emax, sm) : 0.;
 }
 
 // ------------------------------------------------------------------------------
@@ -769,11 +844,13 @@ __device__ __forceinline__ double calc_new_pop(const LvgDevProblem &P, const Lvg
     __syncthreads();
     TACC(PH_LINES, tl0);
     TSTAMP(ta0);
-    double eq = assemble_and_residual(P, M, S.K, S.A, S.y, sm.pold, S.df, sm);
-    TACC(PH_ASSEMBLE, ta0);
+    column_diagonals(P, M, S.K, S.y, sm);
     for (int i = t; i < N; i += BT) sm.bvec[i] = (i == 0) ? 1. : 0.;
     __syncthreads();
-    block_lu_solve(S.A, N, sm.bvec, sm);
+    TACC(PH_ASSEMBLE, ta0);
+    LuSrc src;
+    src.K = S.K; src.y = S.y; src.li = M.line_idx; src.pop = sm.pold; src.df = S.df;
+    const double eq = block_lu_solve<true>(S.A, N, sm.bvec, sm, src);
     for (int i = t; i < N; i += BT) sm.pnew[i] = sm.blog[i];
     __syncthreads();
     return eq;
@@ -915,7 +992,7 @@ __device__ __forceinline__ void boundary_layer_populations(const LvgDevProblem &
     const int N = P.N, t = threadIdx.x;
     for (int i = t; i < N; i += BT) sm.bvec[i] = (i == 0) ? 1. : 0.;
     __syncthreads();
-    block_lu_solve(S.A, N, sm.bvec, sm);   // S.A holds the boundary matrix
+    block_lu_solve<false>(S.A, N, sm.bvec, sm);   // S.A holds the boundary matrix
     for (int i = t; i < N; i += BT) sm.pold[i] = sm.blog[i];
     __syncthreads();
 }
@@ -1000,6 +1077,7 @@ __global__ void __launch_bounds__(BT, 2) solve_kernel(const LvgDevProblem *__res
     __shared__ Smem sm;
     const LvgDevProblem &P = *Pp;
     const LvgLaunch &Lc = *Lp;
+    load_rule_table(P, sm);
     Slot S = make_slot(P, Lc, blockIdx.x);
     for (;;) {
         if (threadIdx.x == 0) sm.layer = atomicAdd(Lc.counter, 1);
@@ -1017,6 +1095,7 @@ __global__ void __launch_bounds__(BT, 2) debug_kernel(const LvgDevProblem *__res
     __shared__ Smem sm;
     const LvgDevProblem &P = *Pp;
     const LvgLaunch &Lc = *Lp;
+    load_rule_table(P, sm);
     Slot S = make_slot(P, Lc, 0);
     const int N = P.N, t = threadIdx.x;
     const LvgModeLines &M = Lc.line_overlap ? P.overlap : P.plain;
@@ -1026,12 +1105,13 @@ __global__ void __launch_bounds__(BT, 2) debug_kernel(const LvgDevProblem *__res
     __syncthreads();
     compute_line_terms(P, M, sm, sm.pold, S.y);
     __syncthreads();
-    double eq = assemble_and_residual(P, M, S.K, S.A, S.y, sm.pold, S.df, sm);
-    for (int e = t; e < N * N; e += BT) Lc.dbg_matrix[e] = S.A[e];
-    for (int i = t; i < N; i += BT) { Lc.dbg_df[i] = S.df[i]; sm.bvec[i] = (i == 0) ? 1. : 0.; }
+    column_diagonals(P, M, S.K, S.y, sm);
+    for (int i = t; i < N; i += BT) sm.bvec[i] = (i == 0) ? 1. : 0.;
     __syncthreads();
-    block_lu_solve(S.A, N, sm.bvec, sm);
-    for (int i = t; i < N; i += BT) Lc.pops[i] = sm.blog[i];
+    LuSrc src;
+    src.K = S.K; src.y = S.y; src.li = M.line_idx; src.pop = sm.pold; src.df = S.df; src.dump = Lc.dbg_matrix;
+    const double eq = block_lu_solve<true>(S.A, N, sm.bvec, sm, src);
+    for (int i = t; i < N; i += BT) { Lc.pops[i] = sm.blog[i]; Lc.dbg_df[i] = S.df[i]; }
     if (t == 0) Lc.dbg_df[N] = eq;
 }
 
