@@ -745,14 +745,15 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             __syncthreads();
             TACC(PH_TRSM, tp2);
             TSTAMP(tp3);
-            // ---- rank-nb update of the rows below (8x8 register tiles)
-            bool ract[8];
+            // ---- rank-nb update of the rows below (8 x TC register tiles). No masks:
+            //      rows that are not below the chunk get l = 0 from the staging, and
+            //      both they and the columns left of jlo are final (stored) already,
+            //      so whatever lands in their registers is never read again.
             bool any = false;
 #pragma unroll
             for (int i = 0; i < 8; i++) {
                 const int pr = 8 * rg + i;
-                ract[i] = pr < N && sm.pos[pr] >= kk + nb;
-                any = any || ract[i];
+                any = any || (pr < N && sm.pos[pr] >= kk + nb);
             }
             if (any && TC * cg + TC - 1 >= jlo) {
                 for (int m = 0; m < nb; m++) {
@@ -764,10 +765,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
 #pragma unroll
                     for (int i = 0; i < 8; i++)
 #pragma unroll
-                        for (int j = 0; j < TC; j++) {
-                            const double r = fma(-a[i], u[j], acc[i][j]);
-                            acc[i][j] = (ract[i] && TC * cg + j >= jlo) ? r : acc[i][j];
-                        }
+                        for (int j = 0; j < TC; j++) acc[i][j] = fma(-a[i], u[j], acc[i][j]);
                 }
             }
             __syncthreads();
