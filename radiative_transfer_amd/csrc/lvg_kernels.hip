@@ -65,8 +65,8 @@ struct Smem {
     int    pos[NMAX];           // its inverse: physical row -> logical position
     double red[8];
     int    ired[8];
-    double pv[2][NB + 2];       // panel pivot-row broadcast, double buffered
-    int    pvi[2][2];
+    double cand[2][NW][NB];     // panel: each wave's pivot candidate row, double buffered
+    int    candp[2][NW];        // its physical row
     double L11[NB][NB + 1];
     double Ub[NB][WB + 2];      // U rows of one chunk across the block column
     union {
@@ -556,31 +556,31 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
             const double wmax = wave_max_dpp(v);
             const int wmin = wave_min_dpp((v == wmax && act) ? lp : 0x7fffffff);
             if ((t & 63) == 0) { sm.red[4 * buf + w] = wmax; sm.ired[4 * buf + w] = wmin; }
-            __syncthreads();
+            if (act && lp == wmin) {               // this wave's candidate publishes its row
+#pragma unroll
+                for (int j = 0; j < NB; j++) if (j >= c) sm.cand[buf][w][j] = rw[j];
+                sm.candp[buf][w] = p;
+            }
+            __syncthreads();                       // one barrier per column
             double vmax = sm.red[4 * buf];
-            int lmin = sm.ired[4 * buf];
+            int lmin = sm.ired[4 * buf], ww = 0;
 #pragma unroll
             for (int i = 1; i < NW; i++) {
                 const double ov = sm.red[4 * buf + i];
                 const int oi = sm.ired[4 * buf + i];
-                if (ov > vmax || (ov == vmax && oi < lmin)) { vmax = ov; lmin = oi; }
+                if (ov > vmax || (ov == vmax && oi < lmin)) { vmax = ov; lmin = oi; ww = i; }
             }
             const bool owner = act && lp == lmin;
-            if (owner) {
-#pragma unroll
-                for (int j = 0; j < NB; j++) if (j >= c) sm.pv[buf][j] = rw[j];
-                sm.pvi[buf][0] = p;
-            }
-            __syncthreads();
-            const double piv = sm.pv[buf][c];
-            const double bc = b[sm.pvi[buf][0]];
+            const double *prow = sm.cand[buf][ww];
+            const double piv = prow[c];
+            const double bc = b[sm.candp[buf][ww]];
             if (owner) { act = false; lp = c; }
             else if (lp == c) lp = lmin;
             if (act) {
                 const double l = rw[c] / piv;
                 rw[c] = l;
 #pragma unroll
-                for (int j = 0; j < NB; j++) if (j > c) rw[j] = fma(-l, sm.pv[buf][j], rw[j]);
+                for (int j = 0; j < NB; j++) if (j > c) rw[j] = fma(-l, prow[j], rw[j]);
                 b[p] = fma(-l, bc, b[p]);
             }
         }
@@ -685,13 +685,25 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                 jlo = kk - c0 + nb;
                 if (jlo >= wJ) break;                  // last chunk of the block column
             } else {
-                for (int e = t; e < NB * NB; e += BT) {
-                    const int r = e / NB, m = e - r * NB;
-                    sm.L11[r][m] = (r < nb && m < r) ? A[(int64_t)sm.perm[kk + r] * N + kk + m] : 0.;
-                }
                 jlo = 0;
             }
+            // L11 of an earlier block's chunk comes from A: load now, store below
+            static_assert(NB * NB <= BT, "one L11 entry per thread");
+            double l11v = 0.;
+            if (kk < c0) {
+                const int r = t / NB, m = t - r * NB;
+                if (t < NB * NB && r < nb && m < r) l11v = A[(int64_t)sm.perm[kk + r] * N + kk + m];
+            }
             TSTAMP(tp2);
+            // ---- L of chunk kk for the rows below it: issue the loads now, land them
+            //      in LDS after the TRSM (their latency hides behind it)
+            const bool lact = t < N && sm.pos[t] >= kk + nb;
+            double lrow[NB];
+            {
+                const double *src_l = A + (int64_t)(lact ? t : 0) * N + kk;
+#pragma unroll
+                for (int m = 0; m < NB; m++) lrow[m] = (lact && m < nb) ? src_l[m] : 0.;
+            }
             // ---- pivot rows of chunk kk (logical kk..kk+nb-1): their current values
             //      in this block column -> Ub (owners write from registers)
 #pragma unroll
@@ -705,6 +717,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                     }
                 }
             }
+            if (kk < c0 && t < NB * NB) sm.L11[t / NB][t % NB] = l11v;
             __syncthreads();
             // ---- TRSM U = L11^-1 Ub: wave w owns columns [WB/4*w, WB/4*(w+1)), lane l row
             //      l&15 of TC/2 of them; x_r takes its updates for m ascending (oracle
@@ -734,14 +747,9 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                     }
                 }
             }
-            // ---- L of chunk kk for the rows below it, transposed into LDS (thread per row)
-            {
-                const int pr = t;
-                const bool lact = pr < N && sm.pos[pr] >= kk + nb;
-                const double *src = A + (int64_t)(lact ? pr : 0) * N + kk;
+            // ---- staged L, transposed (thread per row: conflict-free LDS writes)
 #pragma unroll
-                for (int m = 0; m < NB; m++) sm.pu.LT[m][pr] = (lact && m < nb) ? src[m] : 0.;
-            }
+            for (int m = 0; m < NB; m++) sm.pu.LT[m][t] = lrow[m];
             __syncthreads();
             TACC(PH_TRSM, tp2);
             TSTAMP(tp3);
