@@ -31,7 +31,8 @@ namespace lvg {
 // Diagnostic build only (-DLVG_PHASE_TIMERS): per-phase s_memtime cycle sums,
 // thread 0 of every block, flushed to lvg_phase_cycles[]. Never in the product .so.
 #ifdef LVG_PHASE_TIMERS
-enum { PH_SETUP, PH_BOUNDARY, PH_LINES, PH_ASSEMBLE, PH_PANEL, PH_TRSM, PH_GEMM, PH_BACKSUB, PH_CTL, PH_N };
+enum { PH_SETUP, PH_BOUNDARY, PH_LINES, PH_ASSEMBLE, PH_PANEL, PH_TRSM, PH_GEMM, PH_BACKSUB, PH_CTL,
+       PH_LSETUP, PH_PAIRS, PH_BDIAG, PH_BLOAD, PH_N };
 __device__ unsigned long long lvg_phase_cycles[16];
 #define TSTAMP(v) unsigned long long v = __builtin_amdgcn_s_memtime()
 #define TACC(ph, v0) do { if (threadIdx.x == 0) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
@@ -327,14 +328,22 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
     const double T = sm.T, Te = sm.Te;
     const int nt = (N + 15) >> 4, ntiles = nt * (nt + 1) / 2;
     const int fl = t >> 4, sl = t & 15;
+    TSTAMP(tq0);
     int F = 0, S = 0;
-#pragma unroll 2
+    auto pair_of = [&](int FF, int SS, int &f, int &s) {
+        f = 16 * FF + fl; s = 16 * SS + sl;
+        return (f < N && s < f) ? f * (f - 1) / 2 + s : -1;
+    };
+    int f, s;
+    int pair = pair_of(0, 0, f, s);
+    int cls_next = pair >= 0 ? P.pair_class[pair] : 0;
     for (int q = 0; q < ntiles; q++) {
-        const int f = 16 * F + fl, s = 16 * S + sl;
+        // this tile's pair and class; prefetch the next tile's class
+        const int fc = f, sc = s, pc = pair, cls = cls_next;
         if (++S > F) { S = 0; F++; }
-        if (f >= N || s >= f) continue;
-        const int pair = f * (f - 1) / 2 + s;
-        const int cls = P.pair_class[pair];
+        pair = pair_of(F, S, f, s);
+        cls_next = (q + 1 < ntiles && pair >= 0) ? P.pair_class[pair] : 0;
+        if (pc < 0) continue;
         const int grp = sm.tgrp[cls];
         double dn = 0., gsum = 0.;
         int ng = 0;
@@ -342,30 +351,32 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
         for (int k = 0; k < LVG_MAX_TERMS; k++) {
             const int tb = sm.ttab[cls][k];
             if (tb < 0) break;
-            const double r = table_rate(sm, tb, pair) * sm.cc[sm.tcombo[cls][k]];
+            const double r = table_rate(sm, tb, pc) * sm.cc[sm.tcombo[cls][k]];
             if (k < grp) dn = (k == 0) ? r : dn + r;
             else { gsum = (ng == 0) ? r : gsum + r; ng++; }
         }
         if (ng) dn = dn + gsum;
-        const double de = P.energy[s] - P.energy[f];
+        const double de = P.energy[sc] - P.energy[fc];
         double un = 0.;
-        if (dn > MIN_COLLISION_RATE) un = dn * lvg_exp(de * CM_INVERSE_TO_KELVINS / T) * P.g[f] / P.g[s];
+        if (dn > MIN_COLLISION_RATE) un = dn * lvg_exp(de * CM_INVERSE_TO_KELVINS / T) * P.g[fc] / P.g[sc];
         else dn = 0.;
         double dE = 0., uE = 0.;
         const int et = sm.tet[cls];
         if (et >= 0) {
-            dE = table_rate(sm, et, pair) * sm.ne;
-            if (dE > MIN_COLLISION_RATE) uE = dE * lvg_exp(de * CM_INVERSE_TO_KELVINS / Te) * P.g[f] / P.g[s];
+            dE = table_rate(sm, et, pc) * sm.ne;
+            if (dE > MIN_COLLISION_RATE) uE = dE * lvg_exp(de * CM_INVERSE_TO_KELVINS / Te) * P.g[fc] / P.g[sc];
             else dE = 0.;
         }
-        K[s * N + f] = dn + dE;
-        K[f * N + s] = un + uE;
+        K[sc * N + fc] = dn + dE;
+        K[fc * N + sc] = un + uE;
         if (B) {
-            B[s * N + f] = 0.5 * P.einst[f * N + s] + dn;
-            B[f * N + s] = un;
+            B[sc * N + fc] = 0.5 * P.einst[fc * N + sc] + dn;
+            B[fc * N + sc] = un;
         }
     }
     __syncthreads();
+    TACC(PH_PAIRS, tq0);
+    TSTAMP(tq1);
     if (B) {
         for (int d = t; d < N; d += BT) {
             double a = 0.;
@@ -380,6 +391,7 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
         for (int j = t; j < N; j += BT) B[j] = 1.;   // row 0 <- 1 (iteration_control.cpp:82-84)
         __syncthreads();
     }
+    TACC(PH_BDIAG, tq1);
 }
 
 // ------------------------------------------------------------------------------
@@ -483,12 +495,12 @@ __device__ __forceinline__ void column_diagonals(const LvgDevProblem &P, const L
         const int e1 = M.col_ptr[d + 1];
         int nr = (e < e1) ? M.col_r[e] : N;
         double a = 0.;
-        for (int r0 = 0; r0 < N; r0 += 8) {
-            double kv[8];
+        for (int r0 = 0; r0 < N; r0 += 16) {
+            double kv[16];
 #pragma unroll
-            for (int u = 0; u < 8; u++) kv[u] = (r0 + u < N) ? K[(r0 + u) * N + d] : 0.;
+            for (int u = 0; u < 16; u++) kv[u] = (r0 + u < N) ? K[(r0 + u) * N + d] : 0.;
 #pragma unroll
-            for (int u = 0; u < 8; u++) {
+            for (int u = 0; u < 16; u++) {
                 const int r = r0 + u;
                 if (r < N && r != d) {
                     a = a - kv[u];
@@ -658,7 +670,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                 __syncthreads();
             }
         }
-        TACC(PH_GEMM, tp0);
+        TACC(PH_BLOAD, tp0);
         for (int kk = 0; kk < c0 + wJ; kk += NB) {
             const int nb = min(NB, N - kk);
             int jlo;                                   // first block-local column to update
@@ -721,7 +733,8 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             __syncthreads();
             // ---- TRSM U = L11^-1 Ub: wave w owns columns [WB/4*w, WB/4*(w+1)), lane l row
             //      l&15 of TC/2 of them; x_r takes its updates for m ascending (oracle
-            //      order), x_m broadcast by lane shuffle. U rows to A for back substitution.
+            //      order), x_m broadcast within the 16-lane row by DPP. U rows to A for back
+            //      substitution.
             {
                 const int l = t & 63, w = t >> 6, r = l & 15;
                 double x[TC / 2];
@@ -730,14 +743,22 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                     const int c = (WB / 4) * w + (l >> 4) + 4 * q;
                     x[q] = (r < nb && c < wJ) ? sm.Ub[r][c] : 0.;
                 }
-                for (int m = 0; m < nb - 1; m++) {
-                    const double lm = sm.L11[r][m];
+                double lrw[NB];
 #pragma unroll
-                    for (int q = 0; q < TC / 2; q++) {
-                        const double y = __shfl(x[q], (l & ~15) + m, 64);
-                        if (r > m) x[q] = fma(-lm, y, x[q]);
-                    }
+                for (int m = 0; m < NB; m++) lrw[m] = sm.L11[r][m];
+                // x_m from lane m of each 16-lane row: DPP row_share:m (0x150 + m)
+#define LVG_TRSM_STEP(M_)                                                                  \
+                if ((M_) < nb - 1) {                                                       \
+                    _Pragma("unroll") for (int q = 0; q < TC / 2; q++) {                   \
+                        const double y = dpp_d<0x150 + (M_), 0xf, 0xf>(x[q]);              \
+                        if (r > (M_)) x[q] = fma(-lrw[M_], y, x[q]);                       \
+                    }                                                                      \
                 }
+                LVG_TRSM_STEP(0) LVG_TRSM_STEP(1) LVG_TRSM_STEP(2) LVG_TRSM_STEP(3)
+                LVG_TRSM_STEP(4) LVG_TRSM_STEP(5) LVG_TRSM_STEP(6) LVG_TRSM_STEP(7)
+                LVG_TRSM_STEP(8) LVG_TRSM_STEP(9) LVG_TRSM_STEP(10) LVG_TRSM_STEP(11)
+                LVG_TRSM_STEP(12) LVG_TRSM_STEP(13) LVG_TRSM_STEP(14)
+#undef LVG_TRSM_STEP
                 if (r < nb) {
                     const int64_t prow = (int64_t)sm.perm[kk + r] * N + c0;
 #pragma unroll
@@ -1024,6 +1045,7 @@ __device__ __forceinline__ void solve_layer(const LvgDevProblem &P, const LvgLau
     const LvgModeLines &M = Lc.line_overlap ? P.overlap : P.plain;
     TSTAMP(ts0);
     layer_setup(P, Lc, l, sm);
+    TACC(PH_LSETUP, ts0);
     double *pops = Lc.pops + (int64_t)l * N;
     lvg_layer_status *st = reinterpret_cast<lvg_layer_status *>(Lc.status) + l;
     const bool need_boundary = (Lc.init != LVG_INIT_GIVEN);
