@@ -56,12 +56,14 @@ constexpr double MIN_COLLISION_RATE    = 1.e-99;
 constexpr double INV_TRANS_FACTOR      = -0.1;
 constexpr double MIN_LINE_OPACITY      = 1.e-99;
 
+constexpr int YCAP = 2048;            // line terms kept in LDS when 2*nb_lines <= YCAP
 constexpr int TC = 4;                 // columns per thread in the LU register tile (8 rows x TC)
 constexpr int WB = 8 * TC;            // LU block-column width
 
 struct Smem {
     double pold[NMAX], pnew[NMAX], bvec[NMAX], blog[NMAX];
     double diag[NMAX];          // assembled diagonal of the rate matrix (fused assembly)
+    double ylds[YCAP];          // line terms y of the current iteration (if they fit)
     int    perm[NMAX];          // LU row permutation: logical position -> physical row
     int    pos[NMAX];           // its inverse: physical row -> logical position
     double red[8];
@@ -329,49 +331,72 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
     const int nt = (N + 15) >> 4, ntiles = nt * (nt + 1) / 2;
     const int fl = t >> 4, sl = t & 15;
     TSTAMP(tq0);
+    // batches of PU tiles: indices and classes, then every coefficient load, then
+    // the arithmetic and the stores (loads never wait behind stores that might alias)
+    constexpr int PU = 4;
     int F = 0, S = 0;
-    auto pair_of = [&](int FF, int SS, int &f, int &s) {
-        f = 16 * FF + fl; s = 16 * SS + sl;
-        return (f < N && s < f) ? f * (f - 1) / 2 + s : -1;
-    };
-    int f, s;
-    int pair = pair_of(0, 0, f, s);
-    int cls_next = pair >= 0 ? P.pair_class[pair] : 0;
-    for (int q = 0; q < ntiles; q++) {
-        // this tile's pair and class; prefetch the next tile's class
-        const int fc = f, sc = s, pc = pair, cls = cls_next;
-        if (++S > F) { S = 0; F++; }
-        pair = pair_of(F, S, f, s);
-        cls_next = (q + 1 < ntiles && pair >= 0) ? P.pair_class[pair] : 0;
-        if (pc < 0) continue;
-        const int grp = sm.tgrp[cls];
-        double dn = 0., gsum = 0.;
-        int ng = 0;
+    for (int q0 = 0; q0 < ntiles; q0 += PU) {
+        int pc[PU], fc[PU], sc[PU], cls[PU];
 #pragma unroll
-        for (int k = 0; k < LVG_MAX_TERMS; k++) {
-            const int tb = sm.ttab[cls][k];
-            if (tb < 0) break;
-            const double r = table_rate(sm, tb, pc) * sm.cc[sm.tcombo[cls][k]];
-            if (k < grp) dn = (k == 0) ? r : dn + r;
-            else { gsum = (ng == 0) ? r : gsum + r; ng++; }
+        for (int u = 0; u < PU; u++) {
+            fc[u] = 16 * F + fl; sc[u] = 16 * S + sl;
+            pc[u] = (q0 + u < ntiles && fc[u] < N && sc[u] < fc[u]) ? fc[u] * (fc[u] - 1) / 2 + sc[u] : -1;
+            if (++S > F) { S = 0; F++; }
         }
-        if (ng) dn = dn + gsum;
-        const double de = P.energy[sc] - P.energy[fc];
-        double un = 0.;
-        if (dn > MIN_COLLISION_RATE) un = dn * lvg_exp(de * CM_INVERSE_TO_KELVINS / T) * P.g[fc] / P.g[sc];
-        else dn = 0.;
-        double dE = 0., uE = 0.;
-        const int et = sm.tet[cls];
-        if (et >= 0) {
-            dE = table_rate(sm, et, pc) * sm.ne;
-            if (dE > MIN_COLLISION_RATE) uE = dE * lvg_exp(de * CM_INVERSE_TO_KELVINS / Te) * P.g[fc] / P.g[sc];
-            else dE = 0.;
+#pragma unroll
+        for (int u = 0; u < PU; u++) cls[u] = pc[u] >= 0 ? P.pair_class[pc[u]] : 0;
+        double c0[PU][LVG_MAX_TERMS + 1], c1[PU][LVG_MAX_TERMS + 1];
+#pragma unroll
+        for (int u = 0; u < PU; u++) {
+            bool alive = pc[u] >= 0;
+#pragma unroll
+            for (int k = 0; k <= LVG_MAX_TERMS; k++) {
+                const int tb = (k < LVG_MAX_TERMS) ? sm.ttab[cls[u]][k] : sm.tet[cls[u]];
+                if (k < LVG_MAX_TERMS) alive = alive && tb >= 0;
+                const bool ld = (k < LVG_MAX_TERMS) ? alive : (pc[u] >= 0 && tb >= 0);
+                c0[u][k] = 0.; c1[u][k] = 0.;
+                if (ld) {
+                    const double *c = sm.tcol[tb] + pc[u];
+                    c0[u][k] = c[0];
+                    c1[u][k] = c[sm.timax[tb]];
+                }
+            }
         }
-        K[sc * N + fc] = dn + dE;
-        K[fc * N + sc] = un + uE;
-        if (B) {
-            B[sc * N + fc] = 0.5 * P.einst[fc * N + sc] + dn;
-            B[fc * N + sc] = un;
+#pragma unroll
+        for (int u = 0; u < PU; u++) {
+            if (pc[u] < 0) continue;
+            const int cl = cls[u], f = fc[u], s = sc[u];
+            const int grp = sm.tgrp[cl];
+            double dn = 0., gsum = 0.;
+            int ng = 0;
+#pragma unroll
+            for (int k = 0; k < LVG_MAX_TERMS; k++) {
+                const int tb = sm.ttab[cl][k];
+                if (tb < 0) break;
+                const double deriv = (c1[u][k] - c0[u][k]) / sm.tdt[tb];   // collision_data::get_rate
+                const double r = (c0[u][k] + deriv * sm.tx[tb]) * sm.cc[sm.tcombo[cl][k]];
+                if (k < grp) dn = (k == 0) ? r : dn + r;
+                else { gsum = (ng == 0) ? r : gsum + r; ng++; }
+            }
+            if (ng) dn = dn + gsum;
+            const double de = P.energy[s] - P.energy[f];
+            double un = 0.;
+            if (dn > MIN_COLLISION_RATE) un = dn * lvg_exp(de * CM_INVERSE_TO_KELVINS / T) * P.g[f] / P.g[s];
+            else dn = 0.;
+            double dE = 0., uE = 0.;
+            const int et = sm.tet[cl];
+            if (et >= 0) {
+                const double deriv = (c1[u][LVG_MAX_TERMS] - c0[u][LVG_MAX_TERMS]) / sm.tdt[et];
+                dE = (c0[u][LVG_MAX_TERMS] + deriv * sm.tx[et]) * sm.ne;
+                if (dE > MIN_COLLISION_RATE) uE = dE * lvg_exp(de * CM_INVERSE_TO_KELVINS / Te) * P.g[f] / P.g[s];
+                else dE = 0.;
+            }
+            K[s * N + f] = dn + dE;
+            K[f * N + s] = un + uE;
+            if (B) {
+                B[s * N + f] = 0.5 * P.einst[f * N + s] + dn;
+                B[f * N + s] = un;
+            }
         }
     }
     __syncthreads();
@@ -380,10 +405,15 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
     if (B) {
         for (int d = t; d < N; d += BT) {
             double a = 0.;
-#pragma unroll 8
-            for (int r = 0; r < N; r++) {
-                const double v = B[r * N + d];
-                a = (r != d) ? a - v : a;
+            for (int r0 = 0; r0 < N; r0 += 32) {
+                double bv[32];
+#pragma unroll
+                for (int u = 0; u < 32; u++) bv[u] = (r0 + u < N) ? B[(r0 + u) * N + d] : 0.;
+#pragma unroll
+                for (int u = 0; u < 32; u++) {
+                    const int r = r0 + u;
+                    if (r < N && r != d) a = a - bv[u];
+                }
             }
             B[d * N + d] = a;
         }
@@ -486,29 +516,27 @@ __device__ __forceinline__ void compute_line_terms(const LvgDevProblem &P, const
 // d of K in the reference's order: for partner levels r ascending, -rate(d->r)
 // then, if a line joins d and r, -y (plain scheme); or all collision terms first
 // and the lines after, in line order (overlap scheme). The off-diagonal entries
-// are formed where the LU loads them (block_lu_solve<true>).
+// are formed where the LU loads them (block_lu_solve, fused).
 __device__ __forceinline__ void column_diagonals(const LvgDevProblem &P, const LvgModeLines &M,
                                                  const double *K, const double *y, Smem &sm) {
     const int N = P.N, t = threadIdx.x;
     for (int d = t; d < N; d += BT) {
-        int e = M.col_ptr[d];
-        const int e1 = M.col_ptr[d + 1];
-        int nr = (e < e1) ? M.col_r[e] : N;
         double a = 0.;
         for (int r0 = 0; r0 < N; r0 += 16) {
             double kv[16];
+            int lv[16];
 #pragma unroll
-            for (int u = 0; u < 16; u++) kv[u] = (r0 + u < N) ? K[(r0 + u) * N + d] : 0.;
+            for (int u = 0; u < 16; u++) {
+                const bool ok = r0 + u < N;
+                kv[u] = ok ? K[(r0 + u) * N + d] : 0.;
+                lv[u] = ok ? M.line_idx[(r0 + u) * N + d] : -1;
+            }
 #pragma unroll
             for (int u = 0; u < 16; u++) {
                 const int r = r0 + u;
                 if (r < N && r != d) {
                     a = a - kv[u];
-                    if (r == nr) {
-                        if (M.diag_interleaved) a = a - y[M.col_y[e]];
-                        e++;
-                        nr = (e < e1) ? M.col_r[e] : N;
-                    }
+                    if (M.diag_interleaved && lv[u] >= 0) a = a - y[lv[u]];
                 }
             }
         }
@@ -610,8 +638,7 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
     __syncthreads();
 }
 
-template <bool FUSED>
-__device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Smem &sm, const LuSrc &src = LuSrc()) {
+__device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Smem &sm, const LuSrc &src, const bool FUSED) {
     const int t = threadIdx.x;
     const int rg = t >> 3, cg = t & 7;
     double s_acc = (t == 0) ? 1. : 0.;             // residual row t (FUSED)
@@ -863,26 +890,6 @@ __device__ __forceinline__ double *ring(double *base, int head, int i, int N) {
     return base + (int64_t)((head + i) & (NHIST - 1)) * N;
 }
 
-// calc_new_pop (iteration_lvg.cpp:87-110): sm.pold -> sm.pnew, returns eq_error
-__device__ __forceinline__ double calc_new_pop(const LvgDevProblem &P, const LvgModeLines &M, Slot &S, Smem &sm) {
-    const int N = P.N, t = threadIdx.x;
-    TSTAMP(tl0);
-    compute_line_terms(P, M, sm, sm.pold, S.y);
-    __syncthreads();
-    TACC(PH_LINES, tl0);
-    TSTAMP(ta0);
-    column_diagonals(P, M, S.K, S.y, sm);
-    for (int i = t; i < N; i += BT) sm.bvec[i] = (i == 0) ? 1. : 0.;
-    __syncthreads();
-    TACC(PH_ASSEMBLE, ta0);
-    LuSrc src;
-    src.K = S.K; src.y = S.y; src.li = M.line_idx; src.pop = sm.pold; src.df = S.df;
-    const double eq = block_lu_solve<true>(S.A, N, sm.bvec, sm, src);
-    for (int i = t; i < N; i += BT) sm.pnew[i] = sm.blog[i];
-    __syncthreads();
-    return eq;
-}
-
 // accel_step (iteration_control.h:139-193). Each of the nb_param*nb_param + nb_param
 // sums runs in one thread in the reference's k order; the small system is solved
 // by thread 0 exactly as oracle_lu_solve does.
@@ -948,7 +955,13 @@ __device__ __forceinline__ void accel_step(Ctl &C, Slot &S, int N, Smem &sm) {
 }
 
 // next_step (iteration_control.h:84-137)
-__device__ __forceinline__ void next_step(Ctl &C, const LvgDevProblem &P, const LvgModeLines &M, Slot &S, Smem &sm) {
+
+// calculate_populations (iteration_control.h:196-242); pops in/out in sm.pold
+
+
+// iteration_control::next_step (iteration_control.h:84-137), split around the
+// calc_new_pop solve so that the layer driver has a single LU call site.
+__device__ __forceinline__ void next_step_pre(Ctl &C, const LvgDevProblem &P, Slot &S, Smem &sm) {
     const int N = P.N, t = threadIdx.x;
     // prev_level_pop.push_front(pop_old)
     C.hp = (C.hp + NHIST - 1) & (NHIST - 1);
@@ -960,7 +973,11 @@ __device__ __forceinline__ void next_step(Ctl &C, const LvgDevProblem &P, const 
         accel_step(C, S, N, sm);
         C.nb_after_accel = 0;
     }
-    C.eq_error = calc_new_pop(P, M, S, sm);
+}
+
+__device__ __forceinline__ void next_step_post(Ctl &C, const LvgDevProblem &P, Slot &S, Smem &sm, double eq) {
+    const int N = P.N, t = threadIdx.x;
+    C.eq_error = eq;
     if (C.acceleration && C.iter_nb >= C.accel_start) C.nb_after_accel++;
     const bool better = C.eq_error < C.best_eq;
     if (better) C.best_eq = C.eq_error;
@@ -991,9 +1008,10 @@ __device__ __forceinline__ void next_step(Ctl &C, const LvgDevProblem &P, const 
     __syncthreads();
 }
 
-// calculate_populations (iteration_control.h:196-242); pops in/out in sm.pold
-__device__ __forceinline__ bool calculate_populations(Ctl &C, const LvgDevProblem &P, const LvgModeLines &M,
-                                                      Slot &S, Smem &sm, const LvgLaunch &Lc, int max_nb, int accel) {
+// iteration_control::calculate_populations (iteration_control.h:196-242): state reset
+// of one pass; its iteration loop is the driver loop of solve_layer.
+__device__ __forceinline__ void start_pass(Ctl &C, const LvgDevProblem &P, Slot &S, const LvgLaunch &Lc,
+                                           int max_nb, int accel) {
     const int N = P.N;
     C.acceleration = accel;
     C.accel_start = Lc.accel_start;
@@ -1006,21 +1024,6 @@ __device__ __forceinline__ bool calculate_populations(Ctl &C, const LvgDevProble
     C.hp = C.hr = 0;
     C.np = C.nr = 0;
     for (int i = threadIdx.x; i < N; i += BT) S.opt[i] = 0.;
-    __syncthreads();
-    bool found;
-    do {
-        next_step(C, P, M, S, sm);
-        found = C.rel_error < Lc.min_error;
-    } while (C.iter_nb < C.max_iter && !found);
-    return found;
-}
-
-__device__ __forceinline__ void boundary_layer_populations(const LvgDevProblem &P, Slot &S, Smem &sm) {
-    const int N = P.N, t = threadIdx.x;
-    for (int i = t; i < N; i += BT) sm.bvec[i] = (i == 0) ? 1. : 0.;
-    __syncthreads();
-    block_lu_solve<false>(S.A, N, sm.bvec, sm);   // S.A holds the boundary matrix
-    for (int i = t; i < N; i += BT) sm.pold[i] = sm.blog[i];
     __syncthreads();
 }
 
@@ -1064,28 +1067,60 @@ __device__ __forceinline__ void solve_layer(const LvgDevProblem &P, const LvgLau
     } else if (from_prev) {
         for (int i = t; i < N; i += BT) { sm.pold[i] = pops[i - N]; S.given[i] = pops[i - N]; }
         __syncthreads();
-    } else {
-        TSTAMP(tb0);
-        boundary_layer_populations(P, S, sm);
-        TACC(PH_BOUNDARY, tb0);
-        for (int i = t; i < N; i += BT) S.given[i] = sm.pold[i];
-        __syncthreads();
     }
-    if (Lc.dbg_mode == 2) {
-        for (int i = t; i < N; i += BT) pops[i] = sm.pold[i];
-        return;
-    }
+    // Driver: the boundary-layer solve (iteration_control.cpp:52-91), then the passes of
+    // calculate_populations (accelerated, then the plain retry of radiative_transfer.cpp:
+    // 258-276), all through ONE block_lu_solve call site (one copy of the LU code).
     Ctl C;
     const int accel = Lc.acceleration;
-    bool found = calculate_populations(C, P, M, S, sm, Lc, accel ? Lc.max_iter_acc : Lc.max_iter_plain, accel);
-    int iters = C.iter_nb, retry = 0;
-    // retry without acceleration (radiative_transfer.cpp:258-276)
-    if (!found && accel && Lc.allow_plain_retry) {
-        for (int i = t; i < N; i += BT) sm.pold[i] = S.given[i];
+    const double *yp = (2 * M.nb_lines <= YCAP) ? sm.ylds : S.y;   // line terms in LDS when they fit
+    bool boundary = need_boundary && !from_prev;
+    bool found = false;
+    int iters = 0, retry = 0;
+    if (!boundary) start_pass(C, P, S, Lc, accel ? Lc.max_iter_acc : Lc.max_iter_plain, accel);
+    for (;;) {
+        TSTAMP(tb0);
+        LuSrc src;
+        if (!boundary) {
+            next_step_pre(C, P, S, sm);
+            TSTAMP(tl0);
+            compute_line_terms(P, M, sm, sm.pold, const_cast<double *>(yp));
+            __syncthreads();
+            TACC(PH_LINES, tl0);
+            TSTAMP(ta0);
+            column_diagonals(P, M, S.K, yp, sm);
+            TACC(PH_ASSEMBLE, ta0);
+            src.K = S.K; src.y = yp; src.li = M.line_idx; src.pop = sm.pold; src.df = S.df;
+        }
+        for (int i = t; i < N; i += BT) sm.bvec[i] = (i == 0) ? 1. : 0.;
         __syncthreads();
-        found = calculate_populations(C, P, M, S, sm, Lc, Lc.max_iter_plain, 0);
+        const double eq = block_lu_solve(S.A, N, sm.bvec, sm, src, !boundary);
+        if (boundary) {
+            TACC(PH_BOUNDARY, tb0);
+            for (int i = t; i < N; i += BT) { sm.pold[i] = sm.blog[i]; S.given[i] = sm.blog[i]; }
+            __syncthreads();
+            if (Lc.dbg_mode == 2) {
+                for (int i = t; i < N; i += BT) pops[i] = sm.pold[i];
+                return;
+            }
+            boundary = false;
+            start_pass(C, P, S, Lc, accel ? Lc.max_iter_acc : Lc.max_iter_plain, accel);
+            continue;
+        }
+        for (int i = t; i < N; i += BT) sm.pnew[i] = sm.blog[i];
+        __syncthreads();
+        next_step_post(C, P, S, sm, eq);
+        found = C.rel_error < Lc.min_error;
+        if (C.iter_nb < C.max_iter && !found) continue;
         iters += C.iter_nb;
-        retry = 1;
+        if (!retry && !found && accel && Lc.allow_plain_retry) {
+            retry = 1;
+            for (int i = t; i < N; i += BT) sm.pold[i] = S.given[i];
+            __syncthreads();
+            start_pass(C, P, S, Lc, Lc.max_iter_plain, 0);
+            continue;
+        }
+        break;
     }
     for (int i = t; i < N; i += BT) pops[i] = sm.pold[i];
     if (t == 0) {
@@ -1131,14 +1166,15 @@ __global__ void __launch_bounds__(BT, 2) debug_kernel(const LvgDevProblem *__res
     build_collision_operators(P, sm, S.K, nullptr);
     for (int i = t; i < N; i += BT) sm.pold[i] = Lc.dbg_pop_in[i];
     __syncthreads();
-    compute_line_terms(P, M, sm, sm.pold, S.y);
+    double *yp = (2 * M.nb_lines <= YCAP) ? sm.ylds : S.y;   // line terms in LDS when they fit
+    compute_line_terms(P, M, sm, sm.pold, yp);
     __syncthreads();
-    column_diagonals(P, M, S.K, S.y, sm);
+    column_diagonals(P, M, S.K, yp, sm);
     for (int i = t; i < N; i += BT) sm.bvec[i] = (i == 0) ? 1. : 0.;
     __syncthreads();
     LuSrc src;
-    src.K = S.K; src.y = S.y; src.li = M.line_idx; src.pop = sm.pold; src.df = S.df; src.dump = Lc.dbg_matrix;
-    const double eq = block_lu_solve<true>(S.A, N, sm.bvec, sm, src);
+    src.K = S.K; src.y = yp; src.li = M.line_idx; src.pop = sm.pold; src.df = S.df; src.dump = Lc.dbg_matrix;
+    const double eq = block_lu_solve(S.A, N, sm.bvec, sm, src, true);
     for (int i = t; i < N; i += BT) { Lc.pops[i] = sm.blog[i]; Lc.dbg_df[i] = S.df[i]; }
     if (t == 0) Lc.dbg_df[N] = eq;
 }
