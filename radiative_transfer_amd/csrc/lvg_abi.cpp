@@ -19,6 +19,7 @@
 #include <map>
 #include <string>
 #include <vector>
+#include <cstdlib>
 
 #include "../../include/lvg_amd.h"
 #include "lvg_device.h"
@@ -677,7 +678,12 @@ int lvg_solve_layers_device(lvg_handle *h, int nb_lay, const double *d_soa, doub
     if (nb_lay == 0) return LVG_OK;
     HIPCHECK(h, hipSetDevice(h->device));
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
-    const int grid = std::max(1, std::min(nb_lay, h->cus * h->blocks_per_cu));
+    int per_cu = h->blocks_per_cu;
+    if (const char *e = std::getenv("LVG_BLOCKS_PER_CU")) {   // tuning/diagnostics only
+        const int v = std::atoi(e);
+        if (v >= 1 && v <= h->blocks_per_cu) per_cu = v;
+    }
+    const int grid = std::max(1, std::min(nb_lay, h->cus * per_cu));
     if ((rc = ensure_workspace(h, grid))) return rc;
     LvgLaunch L;
     fill_launch(h, L, o);
