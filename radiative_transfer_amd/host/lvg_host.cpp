@@ -1,0 +1,322 @@
+// lvg_host.cpp — C++ host surface over the C ABI (see lvg_host.hpp).
+#include "lvg_host.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <fstream>
+#include <iostream>
+#include <limits>
+#include <sstream>
+
+namespace lvgamd {
+
+namespace {
+void check(int rc, const lvg_handle *h, const char *what) {
+    if (rc != LVG_OK) {
+        const char *m = lvg_last_error(h);
+        throw lvg_error(rc, std::string(what) + ": " + (m ? m : "error"));
+    }
+}
+
+void skip_lines(std::istream &in, int n) {
+    std::string s;
+    for (int i = 0; i < n; i++) std::getline(in, s);
+}
+}  // namespace
+
+// ---- spectroscopy ---------------------------------------------------------------
+einstein_coeff::einstein_coeff(const energy_diagram *di) : nb_lev(di->nb_lev) {
+    storage.assign((size_t)nb_lev * nb_lev, 0.);
+    rows.resize(nb_lev);
+    for (int i = 0; i < nb_lev; i++) rows[i] = storage.data() + (size_t)i * nb_lev;
+    arr = rows.data();
+}
+
+void einstein_coeff::set_line(int u, int l, double a_ul, const energy_diagram *di) {
+    if (u <= l || u >= nb_lev) throw lvg_error(LVG_E_ARG, "einstein_coeff::set_line: need nb_lev > u > l");
+    arr[u][l] = a_ul;
+    // spectroscopy.cpp:921
+    arr[l][u] = di->lev_array[u].g * arr[u][l] / ((double)di->lev_array[l].g);
+}
+
+// ---- collisions -----------------------------------------------------------------
+collision_data::collision_data(int nb, const std::vector<double> &tg)
+    : imax(nb * (nb - 1) / 2), jmax((int)tg.size()), nb_lev(nb), tgrid(tg) {
+    storage.assign((size_t)imax * jmax, 0.);
+    rows.resize(imax > 0 ? imax : 1);
+    for (int i = 0; i < imax; i++) rows[i] = storage.data() + (size_t)i * jmax;
+    coeff = rows.data();
+}
+
+void collisional_transitions::add_neutral(collision_data *d) {
+    if (nb2 != nb1) throw lvg_error(LVG_E_ARG, "neutral tables must precede electron tables");
+    coll_data.push_back(d);
+    nb1++;
+    nb2++;
+    nb_lev = std::max(nb_lev, d->nb_lev);
+}
+
+void collisional_transitions::add_electron(collision_data *d) {
+    coll_data.push_back(d);
+    nb2++;
+}
+
+collisional_transitions::~collisional_transitions() {
+    for (auto *d : coll_data) delete d;
+}
+
+dust_model::~dust_model() {
+    for (auto *c : components) delete c;
+}
+
+// ---- escape-probability tables ----------------------------------------------------
+// lvg_method_data::lvg_method_data (lvg_method_functions.cpp:21-64)
+lvg_method_data::lvg_method_data(const std::string &path, const std::string &name, int verbosity) {
+    std::ifstream in(path + name);
+    if (!in.is_open()) throw lvg_error(LVG_E_ARG, "lvg_method_data: can't open " + path + name);
+    skip_lines(in, 3);
+    in >> nb_d >> nb_g;
+    if (!in || nb_d < 2 || nb_g < 2) throw lvg_error(LVG_E_ARG, "lvg_method_data: bad header in " + name);
+    delta_arr.resize(nb_d);
+    gamma_arr.resize(nb_g);
+    p.resize((size_t)nb_d * nb_g);
+    for (int i = 0; i < nb_g; i++) in >> gamma_arr[i];
+    for (int i = 0; i < nb_d; i++) {
+        int idx;
+        in >> idx >> delta_arr[i];
+        for (int j = 0; j < nb_g; j++) in >> p[(size_t)i * nb_g + j];
+    }
+    if (!in) throw lvg_error(LVG_E_ARG, "lvg_method_data: truncated " + name);
+    if (verbosity) std::cout << "The data on LVG method have been initialized." << std::endl;
+}
+
+lvg_method_data::lvg_method_data(std::vector<double> delta, std::vector<double> gamma, std::vector<double> pp)
+    : nb_g((int)gamma.size()), nb_d((int)delta.size()), delta_arr(std::move(delta)), gamma_arr(std::move(gamma)),
+      p(std::move(pp)) {
+    if (p.size() != (size_t)nb_d * nb_g) throw lvg_error(LVG_E_ARG, "lvg_method_data: p must be nb_d*nb_g");
+}
+
+void lvg_method_data::save(const std::string &path, const std::string &name) const {
+    std::ofstream out(path + name);
+    if (!out.is_open()) throw lvg_error(LVG_E_ARG, "lvg_method_data::save: can't open " + path + name);
+    out.precision(17);
+    out << "# LVG escape function table\n# written by lvgamd::lvg_method_data::save\n# nb_d nb_g, gamma, rows: idx delta p[nb_g]\n";
+    out << nb_d << " " << nb_g << "\n";
+    for (int i = 0; i < nb_g; i++) out << gamma_arr[i] << (i + 1 < nb_g ? " " : "\n");
+    for (int i = 0; i < nb_d; i++) {
+        out << i << " " << delta_arr[i];
+        for (int j = 0; j < nb_g; j++) out << " " << p[(size_t)i * nb_g + j];
+        out << "\n";
+    }
+}
+
+// lvg_line_overlap_data::lvg_line_overlap_data (lvg_method_functions.cpp:264-313)
+lvg_line_overlap_data::lvg_line_overlap_data(const std::string &path, const std::string &name, int verbosity) {
+    std::ifstream in(path + name);
+    if (!in.is_open()) throw lvg_error(LVG_E_ARG, "lvg_line_overlap_data: can't open " + path + name);
+    skip_lines(in, 3);
+    in >> nb_d >> nb_dx >> nb_gr >> nb_g;
+    if (!in || nb_d < 2 || nb_dx < 2 || nb_gr < 2 || nb_g < 2)
+        throw lvg_error(LVG_E_ARG, "lvg_line_overlap_data: bad header in " + name);
+    log10_delta.resize(nb_d);
+    gamma_arr.resize(nb_g);
+    gratio_arr.resize(nb_gr);
+    dx_arr.resize(nb_dx);
+    p.resize((size_t)nb_dx * nb_d * nb_g * nb_gr);
+    for (int i = 0; i < nb_g; i++) in >> gamma_arr[i];
+    for (int l = 0; l < nb_d; l++)
+        for (int k = 0; k < nb_dx; k++) {
+            double d;
+            in >> d >> dx_arr[k];
+            log10_delta[l] = std::log10(d);   // logarithmic scale on delta (:296)
+            for (int i = 0; i < nb_gr; i++) {
+                int idx;
+                in >> idx >> gratio_arr[i];
+                for (int j = 0; j < nb_g; j++) in >> p[((size_t)l * nb_dx + k) * (nb_g * nb_gr) + i * nb_g + j];
+            }
+        }
+    if (!in) throw lvg_error(LVG_E_ARG, "lvg_line_overlap_data: truncated " + name);
+    if (verbosity) std::cout << "The data on LVG method (line overlaps) have been initialized." << std::endl;
+}
+
+lvg_line_overlap_data::lvg_line_overlap_data(std::vector<double> ld, std::vector<double> dx, std::vector<double> gr,
+                                             std::vector<double> g, std::vector<double> pp)
+    : nb_d((int)ld.size()), nb_dx((int)dx.size()), nb_gr((int)gr.size()), nb_g((int)g.size()),
+      log10_delta(std::move(ld)), dx_arr(std::move(dx)), gratio_arr(std::move(gr)), gamma_arr(std::move(g)),
+      p(std::move(pp)) {
+    if (p.size() != (size_t)nb_d * nb_dx * nb_gr * nb_g) throw lvg_error(LVG_E_ARG, "lvg_line_overlap_data: p size");
+}
+
+// ---- cloud ----------------------------------------------------------------------
+layer_pack::layer_pack(const std::vector<cloud_layer> &lays, int nb_comp) {
+    const int L = (int)lays.size();
+    for (auto &a : f) a.resize(L);
+    dust.assign((size_t)std::max(1, L * nb_comp), 0.);
+    for (int l = 0; l < L; l++) {
+        const cloud_layer &c = lays[l];
+        f[0][l] = c.temp_n;   f[1][l] = c.temp_el;  f[2][l] = c.el_conc; f[3][l] = c.h_conc;
+        f[4][l] = c.ph2_conc; f[5][l] = c.oh2_conc; f[6][l] = c.he_conc; f[7][l] = c.mol_conc;
+        f[8][l] = c.vel_turb; f[9][l] = c.velg_n;
+        if ((int)c.dust_grain_conc.size() < nb_comp)
+            throw lvg_error(LVG_E_ARG, "cloud_layer: dust_grain_conc size must equal dust->nb_of_comp");
+        for (int k = 0; k < nb_comp; k++) dust[(size_t)l * nb_comp + k] = c.dust_grain_conc[k];
+    }
+    view = {L, f[0].data(), f[1].data(), f[2].data(), f[3].data(), f[4].data(), f[5].data(),
+            f[6].data(), f[7].data(), f[8].data(), f[9].data(), dust.data()};
+}
+
+layer_pack::layer_pack(const cloud_data &c, int nb_comp) : layer_pack(c.lay_array, nb_comp) {}
+
+// ---- iteration scheme -----------------------------------------------------------
+iteration_scheme_lvg::iteration_scheme_lvg(const dust_model *d, const lvg_method_data *lf, int verb, int dev)
+    : verbosity(verb), device(dev), dust(d), loss_func(lf) {
+    if (!d || !lf) throw lvg_error(LVG_E_ARG, "iteration_scheme_lvg: dust model and LVG table are required");
+}
+
+iteration_scheme_lvg::~iteration_scheme_lvg() {
+    if (h) lvg_destroy(h);
+}
+
+void iteration_scheme_lvg::init_molecule_data(const energy_diagram *di, const einstein_coeff *ei,
+                                              const collisional_transitions *co) {
+    if (!di || !ei || !co) throw lvg_error(LVG_E_ARG, "init_molecule_data: null argument");
+    const int N = di->nb_lev;
+    diag = di;
+    nb_mol_lev = N;
+    en.resize(N); jj.resize(N); g.resize(N); v.resize(N);
+    for (int i = 0; i < N; i++) {
+        en[i] = di->lev_array[i].energy; jj[i] = di->lev_array[i].j;
+        g[i] = di->lev_array[i].g;       v[i] = di->lev_array[i].v;
+    }
+    mol = {N, di->mol_mass, en.data(), g.data(), v.data(), jj.data(), ei->data()};
+    tabs.clear();
+    for (const collision_data *d : co->coll_data) tabs.push_back({d->nb_lev, d->jmax, d->tgrid.data(), d->data(), d->species});
+    coll = {co->rule(), co->nb1, co->nb2 - co->nb1, tabs.data()};
+    dc.clear();
+    for (const dust_component *c : dust->components)
+        dc.push_back({c->nb_ph_en, c->wvl_exp, c->ph_en_arr.data(), c->abs_coeff.data()});
+    du = {(int)dc.size(), dc.data()};
+    et = {loss_func->nb_d, loss_func->nb_g, loss_func->delta_arr.data(), loss_func->gamma_arr.data(), loss_func->p.data()};
+    if (ov1 && ov2) {
+        o1 = {ov1->nb_d, ov1->nb_dx, ov1->nb_gr, ov1->nb_g, ov1->log10_delta.data(), ov1->dx_arr.data(),
+              ov1->gratio_arr.data(), ov1->gamma_arr.data(), ov1->p.data()};
+        o2 = {ov2->nb_d, ov2->nb_dx, ov2->nb_gr, ov2->nb_g, ov2->log10_delta.data(), ov2->dx_arr.data(),
+              ov2->gratio_arr.data(), ov2->gamma_arr.data(), ov2->p.data()};
+    }
+    prob = {&mol, &coll, &du, &et, (ov1 && ov2) ? &o1 : nullptr, (ov1 && ov2) ? &o2 : nullptr};
+    if (h) { lvg_destroy(h); h = nullptr; }
+    check(lvg_create(&prob, device, &h), nullptr, "lvg_create");
+    if (verbosity) std::cout << "LVG solver tables for " << di->mol_name << " are on device " << device << std::endl;
+}
+
+// set_parameters (iteration_lvg.cpp:59-68): the layer conditions of the next calls
+void iteration_scheme_lvg::set_parameters(double temp_n, double temp_e, double el_conc, double h_conc,
+                                          double ph2_conc, double oh2_conc, double he_conc, double mol_conc,
+                                          double vel_turb) {
+    cur.temp_n = temp_n; cur.temp_el = temp_e; cur.el_conc = el_conc; cur.h_conc = h_conc;
+    cur.ph2_conc = ph2_conc; cur.oh2_conc = oh2_conc; cur.he_conc = he_conc; cur.mol_conc = mol_conc;
+    cur.vel_turb = vel_turb;
+}
+
+// set_dust_parameters (iteration_lvg.cpp:70-85): sizes must match the dust model
+void iteration_scheme_lvg::set_dust_parameters(const std::vector<double> &conc, const std::vector<double> &temp) {
+    if ((int)conc.size() != dust->nb_of_comp || (int)temp.size() != dust->nb_of_comp)
+        throw lvg_error(LVG_E_ARG, "set_dust_parameters: size must equal dust->nb_of_comp");
+    cur.dust_grain_conc = conc;
+    cur.dust_grain_temp = temp;
+}
+
+void iteration_scheme_lvg::calc_new_pop(double *old_pop, double *new_pop, double &eq_error) {
+    if (!h) throw lvg_error(LVG_E_STATE, "calc_new_pop before init_molecule_data");
+    layer_pack lp(std::vector<cloud_layer>{cur}, dust->nb_of_comp);
+    check(lvg_debug_calc_new_pop(h, &lp.view, 0, old_pop, overlap ? 1 : 0, nullptr, nullptr, new_pop, &eq_error), h,
+          "calc_new_pop");
+}
+
+void iteration_scheme_lvg::rate_matrix(const double *pop, double *matrix, double *df) {
+    if (!h) throw lvg_error(LVG_E_STATE, "rate_matrix before init_molecule_data");
+    layer_pack lp(std::vector<cloud_layer>{cur}, dust->nb_of_comp);
+    std::vector<double> pn(nb_mol_lev);
+    double e;
+    check(lvg_debug_calc_new_pop(h, &lp.view, 0, pop, overlap ? 1 : 0, matrix, df, pn.data(), &e), h, "rate_matrix");
+}
+
+iteration_scheme_line_overlap::iteration_scheme_line_overlap(const dust_model *d, const lvg_method_data *lf,
+                                                             const lvg_line_overlap_data *p1,
+                                                             const lvg_line_overlap_data *p2, int verb, int dev)
+    : iteration_scheme_lvg(d, lf, verb, dev) {
+    if (!p1 || !p2) throw lvg_error(LVG_E_ARG, "iteration_scheme_line_overlap: both overlap tables are required");
+    ov1 = p1;
+    ov2 = p2;
+    overlap = true;
+}
+
+// ---- iteration_control -------------------------------------------------------------
+template <class T>
+bool iteration_control<T>::calculate_populations(double *pop, int max_nb_iter, double min_error, bool acceleration,
+                                                 int verbosity) {
+    lvg_solve_opts o;
+    lvg_solve_opts_default(&o);
+    o.min_error = min_error;
+    o.acceleration = acceleration ? 1 : 0;
+    if (acceleration) o.max_iter_acc = max_nb_iter; else o.max_iter_plain = max_nb_iter;
+    o.accel_start = accel_start;
+    o.accel_period = accel_period;
+    o.accel_nb = nb_prev_steps;
+    o.allow_plain_retry = 0;                  // the retry belongs to the layer driver
+    o.init = LVG_INIT_GIVEN;
+    o.line_overlap = scheme->line_overlap() ? 1 : 0;
+    layer_pack lp(std::vector<cloud_layer>{scheme->current_layer()}, (int)scheme->problem().dust->nb_comp);
+    lvg_layer_status st{};
+    check(lvg_solve_layers(scheme->handle(), &lp.view, pop, &o, &st), scheme->handle(), "calculate_populations");
+    iter_nb = st.iterations;
+    eq_error = st.eq_error;
+    pop_error = st.pop_error;
+    rel_error = st.rel_error;
+    if (verbosity) std::cout << "iterations " << iter_nb << " rel_error " << rel_error << std::endl;
+    return st.converged != 0;
+}
+template class iteration_control<iteration_scheme_lvg>;
+template class iteration_control<iteration_scheme_line_overlap>;
+
+// ---- drivers ---------------------------------------------------------------------
+void boundary_layer_populations(iteration_scheme_lvg *s, double *pop, double temp_neutrals, double temp_el,
+                                double el_conc, double h_conc, double ph2_conc, double oh2_conc, double he_conc) {
+    if (!s || !s->handle()) throw lvg_error(LVG_E_STATE, "boundary_layer_populations: scheme not initialised");
+    cloud_layer c = s->current_layer();
+    c.temp_n = temp_neutrals; c.temp_el = temp_el; c.el_conc = el_conc; c.h_conc = h_conc;
+    c.ph2_conc = ph2_conc; c.oh2_conc = oh2_conc; c.he_conc = he_conc;
+    if ((int)c.dust_grain_conc.size() < s->problem().dust->nb_comp) c.dust_grain_conc.assign(s->problem().dust->nb_comp, 0.);
+    layer_pack lp(std::vector<cloud_layer>{c}, s->problem().dust->nb_comp);
+    check(lvg_boundary_layer_populations(s->handle(), &lp.view, pop), s->handle(), "boundary_layer_populations");
+}
+
+std::vector<int> calc_molecular_populations(cloud_data *cloud, iteration_scheme_lvg *it, energy_diagram *mol_levels,
+                                            einstein_coeff *, collisional_transitions *, double *mol_popul,
+                                            int nb_lev, bool acceleration, int verbosity, init_policy init,
+                                            std::vector<lvg_layer_status> *status) {
+    if (!cloud || !it || !it->handle() || !mol_popul) throw lvg_error(LVG_E_ARG, "calc_molecular_populations: bad arguments");
+    if (nb_lev != it->get_vector_dim()) throw lvg_error(LVG_E_ARG, "calc_molecular_populations: nb_lev mismatch");
+    lvg_solve_opts o;
+    lvg_solve_opts_default(&o);
+    o.acceleration = acceleration ? 1 : 0;
+    // radiative_transfer.cpp:259 — no plain retry for methanol
+    o.allow_plain_retry = (mol_levels->mol_name == "CH3OHa" || mol_levels->mol_name == "CH3OHe") ? 0 : 1;
+    o.init = (init == init_policy::warm_chain) ? LVG_INIT_WARM_CHAIN : LVG_INIT_BOUNDARY_LAYER;
+    o.line_overlap = it->line_overlap() ? 1 : 0;
+    layer_pack lp(*cloud, it->problem().dust->nb_comp);
+    std::vector<lvg_layer_status> st(cloud->nb_lay);
+    check(lvg_solve_layers(it->handle(), &lp.view, mol_popul, &o, st.data()), it->handle(), "calc_molecular_populations");
+    std::vector<int> bad;
+    for (int l = 0; l < cloud->nb_lay; l++)
+        if (!st[l].converged) bad.push_back(l);
+    if (verbosity) {
+        std::cout << std::endl << "Can not find solution for layers: " << std::endl;
+        for (int l : bad) std::cout << l << " ";
+        std::cout << std::endl;
+    }
+    if (status) *status = std::move(st);
+    return bad;
+}
+
+}  // namespace lvgamd
