@@ -32,14 +32,19 @@ namespace lvg {
 // thread 0 of every block, flushed to lvg_phase_cycles[]. Never in the product .so.
 #ifdef LVG_PHASE_TIMERS
 enum { PH_SETUP, PH_BOUNDARY, PH_LINES, PH_ASSEMBLE, PH_PANEL, PH_TRSM, PH_GEMM, PH_BACKSUB, PH_CTL,
-       PH_LSETUP, PH_PAIRS, PH_BDIAG, PH_BLOAD, PH_N };
+       PH_LSETUP, PH_PAIRS, PH_BDIAG, PH_BLOAD, PH_CLK_MEMTIME, PH_CLK_REALTIME, PH_N };
 __device__ unsigned long long lvg_phase_cycles[16];
 #define TSTAMP(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#define RSTAMP(v) unsigned long long v = __builtin_amdgcn_s_memrealtime()
+#define RACC(ph, v0) do { if (threadIdx.x == 0) { unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); \
+    atomicAdd(&lvg_phase_cycles[ph], t_ - (v0)); } } while (0)
 #define TACC(ph, v0) do { if (threadIdx.x == 0) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
     atomicAdd(&lvg_phase_cycles[ph], t_ - (v0)); } } while (0)
 #else
 #define TSTAMP(v) do {} while (0)
 #define TACC(ph, v0) do {} while (0)
+#define RSTAMP(v) do {} while (0)
+#define RACC(ph, v0) do {} while (0)
 #endif
 
 constexpr int BT   = 256;   // threads per workgroup
@@ -56,6 +61,12 @@ constexpr double MIN_COLLISION_RATE    = 1.e-99;
 constexpr double INV_TRANS_FACTOR      = -0.1;
 constexpr double MIN_LINE_OPACITY      = 1.e-99;
 
+#ifndef LVG_PREFETCH_L
+#define LVG_PREFETCH_L 0
+#endif
+#ifndef LVG_GEMM_PIPE
+#define LVG_GEMM_PIPE 1
+#endif
 constexpr int YCAP = 2048;            // line terms kept in LDS when 2*nb_lines <= YCAP
 constexpr int TC = 4;                 // columns per thread in the LU register tile (8 rows x TC)
 constexpr int WB = 8 * TC;            // LU block-column width
@@ -698,6 +709,19 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             }
         }
         TACC(PH_BLOAD, tp0);
+        // L rows / L11 entry of the next earlier-block chunk, prefetched during the
+        // current chunk's update (their values are final once the earlier blocks are)
+        double lnext[NB], l11next = 0.;
+        bool have_next = false;
+        auto fetch_l = [&](int k2, double (&lr)[NB], double &l11) {
+            const int nb2 = min(NB, N - k2);
+            const bool la = t < N && sm.pos[t] >= k2 + nb2;
+            const double *src_l = A + (int64_t)(la ? t : 0) * N + k2;
+#pragma unroll
+            for (int m = 0; m < NB; m++) lr[m] = (la && m < nb2) ? src_l[m] : 0.;
+            const int r = t / NB, m = t - r * NB;
+            l11 = (t < NB * NB && r < nb2 && m < r) ? A[(int64_t)sm.perm[k2 + r] * N + k2 + m] : 0.;
+        };
         for (int kk = 0; kk < c0 + wJ; kk += NB) {
             const int nb = min(NB, N - kk);
             int jlo;                                   // first block-local column to update
@@ -726,22 +750,25 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             } else {
                 jlo = 0;
             }
-            // L11 of an earlier block's chunk comes from A: load now, store below
+            // L rows of chunk kk (rows below it) and, for an earlier block's chunk, its
+            // L11 entries: from A, prefetched during the previous step when possible;
+            // for a chunk of this block, from the panel output still in LDS (P). They
+            // land in LDS (LT, which aliases P) after the barrier below.
             static_assert(NB * NB <= BT, "one L11 entry per thread");
-            double l11v = 0.;
-            if (kk < c0) {
-                const int r = t / NB, m = t - r * NB;
-                if (t < NB * NB && r < nb && m < r) l11v = A[(int64_t)sm.perm[kk + r] * N + kk + m];
-            }
+            double l11v = 0., lrow[NB];
             TSTAMP(tp2);
-            // ---- L of chunk kk for the rows below it: issue the loads now, land them
-            //      in LDS after the TRSM (their latency hides behind it)
-            const bool lact = t < N && sm.pos[t] >= kk + nb;
-            double lrow[NB];
-            {
-                const double *src_l = A + (int64_t)(lact ? t : 0) * N + kk;
+            if (kk < c0) {
+                if (have_next) {
 #pragma unroll
-                for (int m = 0; m < NB; m++) lrow[m] = (lact && m < nb) ? src_l[m] : 0.;
+                    for (int m = 0; m < NB; m++) lrow[m] = lnext[m];
+                    l11v = l11next;
+                } else {
+                    fetch_l(kk, lrow, l11v);
+                }
+            } else {
+                const bool la = t < N && sm.pos[t] >= kk + nb;
+#pragma unroll
+                for (int m = 0; m < NB; m++) lrow[m] = (la && m < nb) ? sm.pu.P[la ? t : 0][m] : 0.;
             }
             // ---- pivot rows of chunk kk (logical kk..kk+nb-1): their current values
             //      in this block column -> Ub (owners write from registers)
@@ -799,6 +826,8 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
 #pragma unroll
             for (int m = 0; m < NB; m++) sm.pu.LT[m][t] = lrow[m];
             __syncthreads();
+            have_next = LVG_PREFETCH_L && kk + NB < c0;
+            if (have_next) fetch_l(kk + NB, lnext, l11next);
             TACC(PH_TRSM, tp2);
             TSTAMP(tp3);
             // ---- rank-nb update of the rows below (8 x TC register tiles). No masks:
@@ -812,16 +841,32 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                 any = any || (pr < N && sm.pos[pr] >= kk + nb);
             }
             if (any && TC * cg + TC - 1 >= jlo) {
-                for (int m = 0; m < nb; m++) {
-                    double a[8], u[TC];
+                // operands of step m+1 are read from LDS while step m computes
+                double a0[8], u0[TC], a1[8], u1[TC];
+                auto ld = [&](int m, double (&a)[8], double (&u)[TC]) {
 #pragma unroll
                     for (int i = 0; i < 8; i++) a[i] = sm.pu.LT[m][8 * rg + i];
 #pragma unroll
                     for (int j = 0; j < TC; j++) u[j] = sm.Ub[m][TC * cg + j];
+                };
+                auto upd = [&](const double (&a)[8], const double (&u)[TC]) {
 #pragma unroll
                     for (int i = 0; i < 8; i++)
 #pragma unroll
                         for (int j = 0; j < TC; j++) acc[i][j] = fma(-a[i], u[j], acc[i][j]);
+                };
+                if (LVG_GEMM_PIPE) {
+                    ld(0, a0, u0);
+                    for (int m = 0; m < nb; m += 2) {
+                        if (m + 1 < nb) ld(m + 1, a1, u1);
+                        upd(a0, u0);
+                        if (m + 1 < nb) {
+                            if (m + 2 < nb) ld(m + 2, a0, u0);
+                            upd(a1, u1);
+                        }
+                    }
+                } else {
+                    for (int m = 0; m < nb; m++) { ld(m, a0, u0); upd(a0, u0); }
                 }
             }
             __syncthreads();
@@ -1047,6 +1092,7 @@ __device__ __forceinline__ void solve_layer(const LvgDevProblem &P, const LvgLau
     const int N = P.N, t = threadIdx.x;
     const LvgModeLines &M = Lc.line_overlap ? P.overlap : P.plain;
     TSTAMP(ts0);
+    RSTAMP(rs0);
     layer_setup(P, Lc, l, sm);
     TACC(PH_LSETUP, ts0);
     double *pops = Lc.pops + (int64_t)l * N;
@@ -1132,6 +1178,8 @@ __device__ __forceinline__ void solve_layer(const LvgDevProblem &P, const LvgLau
         st->rel_error = C.rel_error;
         st->pop_error = C.pop_error;
     }
+    TACC(PH_CLK_MEMTIME, ts0);
+    RACC(PH_CLK_REALTIME, rs0);
     __syncthreads();
 }
 

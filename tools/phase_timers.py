@@ -17,9 +17,11 @@ t = time.time(); pops, st = s.solve_layers(L, abi.default_opts(**o)); dt = time.
 ms, _ = s.last_kernel_time()
 lib.lvg_debug_phase_cycles(buf, 1)
 cyc = np.array(buf[:13], dtype=np.float64)
+clk = np.array(buf[13:15], dtype=np.float64)
 its = st["iterations"].sum()
 print(f"{name} layers={nl} kernel {ms:.2f} ms, iterations {its}, LUs {its + nl}")
 tot = cyc[:9].sum() - cyc[1]   # boundary LU overlaps the LU phases
 for n, c in zip(names, cyc):
     print(f"  {n:16s} {c/1e6:10.2f} Mcyc  {100*c/tot:5.1f}%   per-LU {c/(its+nl):10.0f} cyc   per-layer {c/nl:10.0f} cyc")
+print(f"  in-kernel clock (sum memtime / sum realtime x 100 MHz): {clk[0] / max(clk[1], 1) * 0.1:.3f} GHz; busy WG-time {clk[1] / 1e8:.3f} s")
 np.savez(f"/root/repo/gpurun_out/dump_{name}_{nl}.npz", pops=pops, iters=st["iterations"], conv=st["converged"])
