@@ -240,6 +240,51 @@ int         lvg_debug_calc_new_pop(lvg_handle *h, const lvg_layers *layers, int 
 int         lvg_boundary_layer_populations(lvg_handle *h, const lvg_layers *layers,
                                            double *pops_out);
 
+/* ---- post-processing of the populations ------------------------------------
+ * transition_data_container::find (transition_data.cpp:380-417) with calc_inv,
+ * calc_gain, calc_line_profile and calc_exc_temp (:210-377), on the device.
+ * Lines are the (u > l) pairs with A_ul != 0 in (u, l) ascending order; a line is
+ * kept when some layer has inv * g_u > rel_error * pops[u] (the reference compares
+ * with the FIRST layer's population of u, level_pop[i], :398 — reproduced) and then
+ * tau_max >= min_optical_depth. Results come in the order of the reference's list
+ * (push_front: last found first). */
+#define LVG_NB_ASPECT 37    /* transition_data::nb_aspect_ratio (transition_data.cpp:18) */
+#define LVG_NB_FREQ   300   /* transition_data::nb_freq                                  */
+
+typedef struct lvg_cloud_geometry {
+    const double *dz;      /* [nb_lay] cloud_layer::dz, cm                           */
+    const double *vel_n;   /* [nb_lay] cloud_layer::vel_n, cm/s                      */
+    double height;         /* cloud_data::get_height() = zu(last) - zl(first) (cloud_data.cpp:106) */
+} lvg_cloud_geometry;
+
+typedef struct lvg_find_opts {
+    double rel_error;           /* find(level_pop, rel_error)                         */
+    double min_optical_depth;   /* 0.01 (transition_data.cpp:182)                     */
+    double velocity_shift;      /* 5e5 cm/s (:190)                                    */
+    double delta_aspect_ratio;  /* 0.25 (:18)                                         */
+    int    h2o22_up, h2o22_low; /* levels of the o-H2O 6_16-5_23 22 GHz line, whose gain
+                                   width includes the hyperfine spread (:251-263); -1: none */
+} lvg_find_opts;
+
+typedef struct lvg_transition {
+    int    up, low;             /* level indices                                     */
+    int    lay_nb_hg;           /* layer of the highest gain (0 if none positive)    */
+    int    reserved;
+    double energy;              /* E_up - E_low, cm^-1                               */
+    double inv, gain;           /* dz-weighted averages over the cloud               */
+    double tau_eff, tau_max;
+    double tau_vs_aspect_ratio[LVG_NB_ASPECT];
+    double tau_vs_frequency[LVG_NB_FREQ];
+} lvg_transition;
+
+void        lvg_find_opts_default(lvg_find_opts *o);
+/* pops: host [nb_lay*N]. out: [max_out]; inv_arr, gain_arr, exc_temp_arr: host
+ * [max_out*nb_lay] (row k belongs to out[k]) or NULL. *nb_out receives the number of
+ * transitions found even when it exceeds max_out (then only max_out are written). */
+int         lvg_find_transitions(lvg_handle *h, const lvg_layers *layers, const lvg_cloud_geometry *geo,
+                                 const double *pops, const lvg_find_opts *opts, int max_out, int *nb_out,
+                                 lvg_transition *out, double *inv_arr, double *gain_arr, double *exc_temp_arr);
+
 /* Kernel timing of the last lvg_solve_layers* call on this handle, measured
  * with HIP events on the stream the kernels ran on: total milliseconds of the
  * solve kernel(s) and their count. */

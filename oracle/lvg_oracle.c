@@ -968,5 +968,183 @@ int oracle_nb_overlap_lines(const lvg_problem *P, double vel_width, int *nb_doub
 }
 
 /* probes of the shared elementary functions (tests compare them with libm) */
+/* ------------------------------------------------------------------------ */
+/* transition_data_container (transition_data.cpp:181-417): post-processing   */
+/* ------------------------------------------------------------------------ */
+#define ONEDIVBY_SQRT_PI 0.56418958354775628  /* constants.h (absent): 1/sqrt(pi) */
+
+void oracle_find_opts_default(lvg_find_opts *o)
+{
+    o->rel_error = 1.e-5;
+    o->min_optical_depth = 0.01;      /* transition_data.cpp:182 */
+    o->velocity_shift = 5.e+5;        /* :190 */
+    o->delta_aspect_ratio = 0.25;     /* :18 */
+    o->h2o22_up = o->h2o22_low = -1;
+}
+
+typedef struct {
+    int up, low;
+    double energy, inv, gain, tau_eff, tau_max;
+    int lay_nb_hg;
+    double *inv_arr, *gain_arr, *exc_temp_arr, tau_asp[LVG_NB_ASPECT], tau_freq[LVG_NB_FREQ];
+} otrans_t;
+
+/* calc_inv (:210-223) */
+static void o_calc_inv(otrans_t *t, const lvg_problem *P, const lvg_cloud_geometry *G, int nlay, const double *pop)
+{
+    const int N = P->mol->nb_lev;
+    t->inv = 0.;
+    for (int lay = 0; lay < nlay; lay++) {
+        double low_pop = pop[lay * N + t->low], up_pop = pop[lay * N + t->up];
+        t->inv_arr[lay] = up_pop / P->mol->g[t->up] - low_pop / P->mol->g[t->low];
+        t->inv += t->inv_arr[lay] * G->dz[lay];
+    }
+    t->inv /= G->height;
+}
+
+/* calc_exc_temp (:225-238), log from lvg_math.h */
+static void o_calc_exc_temp(otrans_t *t, const lvg_problem *P, int nlay, const double *pop)
+{
+    const int N = P->mol->nb_lev;
+    for (int lay = 0; lay < nlay; lay++) {
+        double low_pop = pop[lay * N + t->low], up_pop = pop[lay * N + t->up];
+        t->exc_temp_arr[lay] = CM_INVERSE_TO_KELVINS * t->energy
+            / lvg_log((low_pop * P->mol->g[t->up]) / (up_pop * P->mol->g[t->low]));
+    }
+}
+
+/* calc_gain (:240-294); pow(x, 0.5) -> sqrt, pow(x, 2.) -> x*x (DESIGN.md "Parity") */
+static void o_calc_gain(otrans_t *t, const lvg_problem *P, const lvg_layers *L, const lvg_cloud_geometry *G,
+                        const lvg_find_opts *o)
+{
+    const int N = P->mol->nb_lev, nlay = L->nb_lay, nc = P->dust ? P->dust->nb_comp : 0;
+    const int h2o22 = (t->up == o->h2o22_up && t->low == o->h2o22_low);
+    const double energy = t->energy, energy_th = energy * energy * energy;
+    const double aul = P->mol->einst[t->up * N + t->low];
+    for (int lay = 0; lay < nlay; lay++) {
+        double vel, vt = L->vel_turb[lay];
+        if (h2o22) {
+            double a = sqrt(2. * BOLTZMANN_CONSTANT * L->temp_n[lay] / P->mol->mass) + 5.e+4;
+            vel = sqrt(a * a + vt * vt);
+        } else {
+            vel = sqrt(2. * BOLTZMANN_CONSTANT * L->temp_n[lay] / P->mol->mass + vt * vt);
+        }
+        double line_gain = t->inv_arr[lay] * P->mol->g[t->up] * aul * ONEDIVBY_SQRT_PI * L->mol_conc[lay]
+            / (energy_th * EIGHT_PI * vel);
+        double d_abs = nc ? oracle_dust_absorption(P->dust, energy, L->dust_conc + (size_t)lay * nc) : 0.;
+        t->gain_arr[lay] = line_gain - d_abs;
+    }
+    double g = 0.;
+    t->gain = t->tau_eff = 0.;
+    t->lay_nb_hg = 0;
+    for (int lay = 0; lay < nlay; lay++) {
+        t->gain += t->gain_arr[lay] * G->dz[lay];
+        if (t->gain_arr[lay] > 0.) t->tau_eff += t->gain_arr[lay] * G->dz[lay];
+        if (t->gain_arr[lay] > g) { g = t->gain_arr[lay]; t->lay_nb_hg = lay; }
+    }
+    t->gain /= G->height;
+    if (g < 1.e-99) t->lay_nb_hg = 0;
+}
+
+/* calc_line_profile (:296-378), exp from lvg_math.h */
+static void o_calc_line_profile(otrans_t *t, const lvg_problem *P, const lvg_layers *L, const lvg_cloud_geometry *G,
+                                const lvg_find_opts *o)
+{
+    const int N = P->mol->nb_lev, nlay = L->nb_lay, nc = P->dust ? P->dust->nb_comp : 0;
+    const double energy = t->energy, energy_th = energy * energy * energy;
+    const double aul = P->mol->einst[t->up * N + t->low];
+    const double vmax = G->vel_n[0] + o->velocity_shift, vmin = G->vel_n[nlay - 1] - o->velocity_shift;
+    const double dv = (vmax - vmin) / (LVG_NB_FREQ - 1.);
+    double *lo = (double *)malloc(sizeof(double) * nlay * 3), *vw = lo + nlay, *dop = vw + nlay;
+    double *od = (double *)malloc(sizeof(double) * LVG_NB_FREQ * LVG_NB_ASPECT);
+    for (int lay = 0; lay < nlay; lay++) {
+        double vt = L->vel_turb[lay];
+        vw[lay] = sqrt(2. * BOLTZMANN_CONSTANT * L->temp_n[lay] / P->mol->mass + vt * vt);
+        lo[lay] = t->inv_arr[lay] * P->mol->g[t->up] * aul * L->mol_conc[lay] * ONEDIVBY_SQRT_PI
+            / (energy_th * EIGHT_PI * vw[lay]);
+        dop[lay] = nc ? oracle_dust_absorption(P->dust, energy, L->dust_conc + (size_t)lay * nc) : 0.;
+    }
+    for (int i = 0; i < LVG_NB_ASPECT; i++) {
+        double aspect_ratio = 1. + o->delta_aspect_ratio * i;
+        double vel = vmin;
+        for (int n = 0; n < LVG_NB_FREQ; vel += dv, n++) {
+            double acc = 0.;
+            for (int lay = 0; lay < nlay; lay++) {
+                double x = (vel - G->vel_n[lay] / aspect_ratio) / vw[lay];
+                double profile = lvg_exp(-x * x);
+                if (lo[lay] * profile - dop[lay] > 0.)
+                    acc += (lo[lay] * profile - dop[lay]) * G->dz[lay] * aspect_ratio;
+            }
+            od[n * LVG_NB_ASPECT + i] = acc;
+        }
+    }
+    for (int i = 0; i < LVG_NB_ASPECT; i++) {
+        double x = 0.;
+        for (int n = 0; n < LVG_NB_FREQ; n++)
+            if (x < od[n * LVG_NB_ASPECT + i]) x = od[n * LVG_NB_ASPECT + i];
+        t->tau_asp[i] = x;
+    }
+    t->tau_max = t->tau_asp[0];
+    for (int n = 0; n < LVG_NB_FREQ; n++) t->tau_freq[n] = od[n * LVG_NB_ASPECT];
+    free(od);
+    free(lo);
+}
+
+/* find (:380-417). Output in the reference's list order (push_front). */
+int oracle_find_transitions(const lvg_problem *P, const lvg_layers *L, const lvg_cloud_geometry *G,
+                            const double *pops, const lvg_find_opts *o, int max_out, int *nb_out,
+                            lvg_transition *out, double *inv_arr, double *gain_arr, double *exc_temp_arr)
+{
+    const int N = P->mol->nb_lev, nlay = L->nb_lay;
+    if (nlay < 1) { *nb_out = 0; return 0; }
+    int cap = 16, nf = 0;
+    otrans_t *found = (otrans_t *)malloc(sizeof(otrans_t) * cap);
+    otrans_t t;
+    t.inv_arr = (double *)malloc(sizeof(double) * nlay * 3);
+    t.gain_arr = t.inv_arr + nlay;
+    t.exc_temp_arr = t.gain_arr + nlay;
+    for (int i = 1; i < N; i++)
+        for (int j = 0; j < i; j++) {
+            if (P->mol->einst[i * N + j] == 0.) continue;
+            t.up = i; t.low = j;
+            t.energy = P->mol->energy[i] - P->mol->energy[j];
+            o_calc_inv(&t, P, G, nlay, pops);
+            int inverted = 0;
+            for (int lay = 0; lay < nlay; lay++) {
+                inverted = (t.inv_arr[lay] * P->mol->g[i] > o->rel_error * pops[i]);   /* level_pop[i]: layer 0 (:398) */
+                if (inverted) break;
+            }
+            if (!inverted) continue;
+            o_calc_gain(&t, P, L, G, o);
+            o_calc_line_profile(&t, P, L, G, o);
+            if (t.tau_max >= o->min_optical_depth) {
+                o_calc_exc_temp(&t, P, nlay, pops);
+                if (nf == cap) { cap *= 2; found = (otrans_t *)realloc(found, sizeof(otrans_t) * cap); }
+                found[nf] = t;
+                found[nf].inv_arr = (double *)malloc(sizeof(double) * nlay * 3);
+                memcpy(found[nf].inv_arr, t.inv_arr, sizeof(double) * nlay * 3);
+                found[nf].gain_arr = found[nf].inv_arr + nlay;
+                found[nf].exc_temp_arr = found[nf].gain_arr + nlay;
+                nf++;
+            }
+        }
+    *nb_out = nf;
+    for (int k = 0; k < nf && k < max_out; k++) {
+        const otrans_t *f = &found[nf - 1 - k];
+        lvg_transition *r = &out[k];
+        r->up = f->up; r->low = f->low; r->lay_nb_hg = f->lay_nb_hg; r->reserved = 0;
+        r->energy = f->energy; r->inv = f->inv; r->gain = f->gain; r->tau_eff = f->tau_eff; r->tau_max = f->tau_max;
+        memcpy(r->tau_vs_aspect_ratio, f->tau_asp, sizeof f->tau_asp);
+        memcpy(r->tau_vs_frequency, f->tau_freq, sizeof f->tau_freq);
+        if (inv_arr) memcpy(inv_arr + (size_t)k * nlay, f->inv_arr, sizeof(double) * nlay);
+        if (gain_arr) memcpy(gain_arr + (size_t)k * nlay, f->gain_arr, sizeof(double) * nlay);
+        if (exc_temp_arr) memcpy(exc_temp_arr + (size_t)k * nlay, f->exc_temp_arr, sizeof(double) * nlay);
+    }
+    for (int k = 0; k < nf; k++) free(found[k].inv_arr);
+    free(found);
+    free(t.inv_arr);
+    return 0;
+}
+
 double oracle_exp(double x) { return lvg_exp(x); }
 double oracle_log10(double x) { return lvg_log10(x); }

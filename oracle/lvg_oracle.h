@@ -25,6 +25,10 @@ double oracle_overlap_esc_func(const lvg_overlap_table *T, double gamma, double 
                                double gamma_ratio, double delta_x);
 double oracle_dust_absorption(const lvg_dust *d, double energy, const double *conc);
 int    oracle_lu_solve(double *a, double *b, int n);
+void   oracle_find_opts_default(lvg_find_opts *o);
+int    oracle_find_transitions(const lvg_problem *P, const lvg_layers *L, const lvg_cloud_geometry *G,
+                               const double *pops, const lvg_find_opts *o, int max_out, int *nb_out,
+                               lvg_transition *out, double *inv_arr, double *gain_arr, double *exc_temp_arr);
 double oracle_exp(double x);
 double oracle_log10(double x);
 #ifdef __cplusplus

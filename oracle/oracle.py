@@ -54,6 +54,7 @@ def lib():
         L.oracle_dust_absorption.argtypes = [vp, d, dp]
         L.oracle_dust_absorption.restype = d
         L.oracle_lu_solve.argtypes = [dp, dp, i]
+        L.oracle_find_transitions.argtypes = [vp, vp, vp, dp, vp, i, C.POINTER(C.c_int), vp, dp, dp, dp]
         L.oracle_exp.argtypes = [d]
         L.oracle_exp.restype = d
         L.oracle_log10.argtypes = [d]
@@ -129,3 +130,24 @@ def lu_solve(a, b):
     b = np.array(b, dtype=np.float64, copy=True)
     lib().oracle_lu_solve(abi.dptr(a), abi.dptr(b), b.size)
     return b
+
+
+def find_transitions(prob, layers, geo, pops, opts=None, max_out: int = 256):
+    """oracle_find_transitions: same outputs as LvgSolver.find_transitions."""
+    cp, cl = prob.to_c(), layers.to_c()
+    cg = geo.to_c()
+    o = opts if opts is not None else abi.find_opts()
+    p = np.ascontiguousarray(pops, dtype=np.float64)
+    nl = layers.nb_lay
+    while True:
+        out = np.zeros(max_out, dtype=abi.TRANSITION_DTYPE)
+        inv = np.zeros((max_out, nl)); gain = np.zeros((max_out, nl)); exc = np.zeros((max_out, nl))
+        n = C.c_int()
+        rc = lib().oracle_find_transitions(cp.ptr, cl.ptr, C.byref(cg), abi.dptr(p), C.byref(o), max_out, C.byref(n),
+                                           out.ctypes.data_as(C.c_void_p), abi.dptr(inv), abi.dptr(gain), abi.dptr(exc))
+        assert rc == 0
+        if n.value <= max_out:
+            k = n.value
+            return out[:k].copy(), inv[:k].copy(), gain[:k].copy(), exc[:k].copy()
+        max_out = n.value
+

@@ -272,6 +272,47 @@ class CLayers:
         return C.byref(self.s)
 
 
+# ---- post-processing (transition_data_container::find) ---------------------------------
+NB_ASPECT = 37
+NB_FREQ = 300
+
+
+class c_cloud_geometry(C.Structure):
+    _fields_ = [("dz", _dp), ("vel_n", _dp), ("height", C.c_double)]
+
+
+class c_find_opts(C.Structure):
+    _fields_ = [("rel_error", C.c_double), ("min_optical_depth", C.c_double), ("velocity_shift", C.c_double),
+                ("delta_aspect_ratio", C.c_double), ("h2o22_up", C.c_int), ("h2o22_low", C.c_int)]
+
+
+TRANSITION_DTYPE = np.dtype([("up", np.int32), ("low", np.int32), ("lay_nb_hg", np.int32), ("reserved", np.int32),
+                             ("energy", np.float64), ("inv", np.float64), ("gain", np.float64),
+                             ("tau_eff", np.float64), ("tau_max", np.float64),
+                             ("tau_vs_aspect_ratio", np.float64, (NB_ASPECT,)),
+                             ("tau_vs_frequency", np.float64, (NB_FREQ,))])
+
+
+def find_opts(**kw) -> c_find_opts:
+    o = c_find_opts(1e-5, 0.01, 5e5, 0.25, -1, -1)
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
+@dataclass
+class Geometry:
+    """cloud_layer::dz / vel_n and cloud_data::get_height() (cloud_data.h:27-29, .cpp:106)."""
+    dz: np.ndarray
+    vel_n: np.ndarray
+    height: float
+
+    def to_c(self):
+        self._dz = np.ascontiguousarray(self.dz, dtype=np.float64)
+        self._vel = np.ascontiguousarray(self.vel_n, dtype=np.float64)
+        return c_cloud_geometry(dptr(self._dz), dptr(self._vel), float(self.height))
+
+
 def default_opts(**kw) -> c_solve_opts:
     o = c_solve_opts(1e-5, 150, 15000, 40, 5, 5, 1, 1, LVG_INIT_BOUNDARY_LAYER, 0)
     for k, v in kw.items():

@@ -28,6 +28,7 @@ extern "C" hipError_t lvg_launch_solve(const LvgDevProblem *P, const LvgLaunch *
 extern "C" hipError_t lvg_launch_debug(const LvgDevProblem *P, const LvgLaunch *L, hipStream_t s);
 extern "C" int lvg_kernel_max_levels(void);
 extern "C" hipError_t lvg_kernel_occupancy(int *blocks_per_cu);
+extern "C" hipError_t lvg_tr_launch(int stage, const void *args_dev, int nb_lines, int nb_lay, int nb_sel, hipStream_t s);
 
 namespace {
 
@@ -874,3 +875,118 @@ int lvg_boundary_layer_populations(lvg_handle *h, const lvg_layers *layers, doub
 }
 
 }  // extern "C"
+
+// ---- post-processing: transition_data_container::find --------------------------------
+namespace {
+struct TmpDev {   // call-scoped device buffers
+    std::vector<void *> ptrs;
+    ~TmpDev() { for (void *p : ptrs) (void)hipFree(p); }
+    template <class T> T *alloc(size_t n) {
+        void *p = nullptr;
+        if (hipMalloc(&p, std::max<size_t>(1, n) * sizeof(T)) != hipSuccess) return nullptr;
+        ptrs.push_back(p);
+        return static_cast<T *>(p);
+    }
+};
+}  // namespace
+
+void lvg_find_opts_default(lvg_find_opts *o) {
+    if (!o) return;
+    o->rel_error = 1.e-5;
+    o->min_optical_depth = 0.01;    // transition_data.cpp:182
+    o->velocity_shift = 5.e+5;      // :190
+    o->delta_aspect_ratio = 0.25;   // :18
+    o->h2o22_up = o->h2o22_low = -1;
+}
+
+int lvg_find_transitions(lvg_handle *h, const lvg_layers *layers, const lvg_cloud_geometry *geo, const double *pops,
+                         const lvg_find_opts *opts, int max_out, int *nb_out, lvg_transition *out, double *inv_arr,
+                         double *gain_arr, double *exc_temp_arr) {
+    if (!h) return LVG_E_STATE;
+    if (!layers || !geo || !opts || !nb_out || max_out < 0 || (max_out > 0 && !out))
+        return fail(h, LVG_E_ARG, "lvg_find_transitions: missing argument");
+    *nb_out = 0;
+    const int nl = layers->nb_lay, N = h->N, nlines = h->P.plain.nb_lines;
+    if (nl == 0 || nlines == 0) return LVG_OK;
+    if (!pops || !geo->dz || !geo->vel_n) return fail(h, LVG_E_ARG, "lvg_find_transitions: pops / dz / vel_n missing");
+    HIPCHECK(h, hipSetDevice(h->device));
+    int rc = upload_layers(h, layers);
+    if (rc) return rc;
+    TmpDev T;
+    const size_t nll = (size_t)nlines * nl;
+    double *d_pops = T.alloc<double>((size_t)nl * N), *d_dz = T.alloc<double>(nl), *d_vel = T.alloc<double>(nl);
+    double *d_inv = T.alloc<double>(nll), *d_gain = T.alloc<double>(nll), *d_exc = T.alloc<double>(nll);
+    double *d_lop = T.alloc<double>(nll), *d_dop = T.alloc<double>(nll), *d_vw = T.alloc<double>(nl);
+    double *d_sum = T.alloc<double>(4 * (size_t)nlines);
+    int *d_inverted = T.alloc<int>(nlines);
+    lvgtr::TrArgs *d_args = T.alloc<lvgtr::TrArgs>(1);
+    if (!d_pops || !d_dz || !d_vel || !d_inv || !d_gain || !d_exc || !d_lop || !d_dop || !d_vw || !d_sum ||
+        !d_inverted || !d_args)
+        return fail(h, LVG_E_NOMEM, "lvg_find_transitions: device allocation failed");
+    HIPCHECK(h, hipMemcpy(d_pops, pops, sizeof(double) * (size_t)nl * N, hipMemcpyHostToDevice));
+    HIPCHECK(h, hipMemcpy(d_dz, geo->dz, sizeof(double) * nl, hipMemcpyHostToDevice));
+    HIPCHECK(h, hipMemcpy(d_vel, geo->vel_n, sizeof(double) * nl, hipMemcpyHostToDevice));
+    HIPCHECK(h, hipMemset(d_inverted, 0, sizeof(int) * nlines));
+    const LvgModeLines &M = h->P.plain;
+    lvgtr::TrArgs a{};
+    a.N = N; a.nb_lines = nlines; a.nb_lay = nl; a.nb_comp = h->nb_comp; a.soa_ld = nl;
+    a.line_u = M.line_u; a.line_l = M.line_l; a.line_aul = M.line_aul; a.line_e = M.line_e; a.line_sigma = M.line_sigma;
+    a.g = h->P.g; a.mass = h->P.mass;
+    a.soa = h->d_soa; a.pops = d_pops; a.dz = d_dz; a.vel_n = d_vel;
+    a.height = geo->height; a.rel_error = opts->rel_error; a.velocity_shift = opts->velocity_shift;
+    a.delta_aspect = opts->delta_aspect_ratio; a.h2o22_up = opts->h2o22_up; a.h2o22_low = opts->h2o22_low;
+    a.inv = d_inv; a.gain = d_gain; a.exc = d_exc; a.lop = d_lop; a.dop = d_dop; a.vw = d_vw;
+    a.inverted = d_inverted; a.line_sum = d_sum;
+    HIPCHECK(h, hipMemcpy(d_args, &a, sizeof a, hipMemcpyHostToDevice));
+    HIPCHECK(h, lvg_tr_launch(0, d_args, nlines, nl, 0, h->stream));
+    std::vector<int> inverted(nlines), lu(nlines), ll(nlines);
+    std::vector<double> sums(4 * (size_t)nlines), le(nlines);
+    HIPCHECK(h, hipStreamSynchronize(h->stream));
+    HIPCHECK(h, hipMemcpy(inverted.data(), d_inverted, sizeof(int) * nlines, hipMemcpyDeviceToHost));
+    HIPCHECK(h, hipMemcpy(sums.data(), d_sum, sizeof(double) * sums.size(), hipMemcpyDeviceToHost));
+    HIPCHECK(h, hipMemcpy(lu.data(), M.line_u, sizeof(int) * nlines, hipMemcpyDeviceToHost));
+    HIPCHECK(h, hipMemcpy(ll.data(), M.line_l, sizeof(int) * nlines, hipMemcpyDeviceToHost));
+    HIPCHECK(h, hipMemcpy(le.data(), M.line_e, sizeof(double) * nlines, hipMemcpyDeviceToHost));
+    std::vector<int> sel;
+    for (int n = 0; n < nlines; n++)
+        if (inverted[n]) sel.push_back(n);
+    const int nsel = (int)sel.size();
+    if (nsel == 0) return LVG_OK;
+    int *d_sel = T.alloc<int>(nsel);
+    double *d_od = T.alloc<double>((size_t)nsel * LVG_NB_FREQ * LVG_NB_ASPECT);
+    double *d_asp = T.alloc<double>((size_t)nsel * LVG_NB_ASPECT), *d_freq = T.alloc<double>((size_t)nsel * LVG_NB_FREQ);
+    if (!d_sel || !d_od || !d_asp || !d_freq) return fail(h, LVG_E_NOMEM, "lvg_find_transitions: device allocation failed");
+    HIPCHECK(h, hipMemcpy(d_sel, sel.data(), sizeof(int) * nsel, hipMemcpyHostToDevice));
+    a.sel = d_sel; a.nb_sel = nsel; a.od = d_od; a.tau_asp = d_asp; a.tau_freq = d_freq;
+    HIPCHECK(h, hipMemcpy(d_args, &a, sizeof a, hipMemcpyHostToDevice));
+    HIPCHECK(h, lvg_tr_launch(1, d_args, nlines, nl, nsel, h->stream));
+    HIPCHECK(h, hipStreamSynchronize(h->stream));
+    std::vector<double> asp((size_t)nsel * LVG_NB_ASPECT), freq((size_t)nsel * LVG_NB_FREQ);
+    HIPCHECK(h, hipMemcpy(asp.data(), d_asp, sizeof(double) * asp.size(), hipMemcpyDeviceToHost));
+    HIPCHECK(h, hipMemcpy(freq.data(), d_freq, sizeof(double) * freq.size(), hipMemcpyDeviceToHost));
+    std::vector<int> kept;   // indices into sel, in line order (tau_max >= min_optical_depth)
+    for (int k = 0; k < nsel; k++)
+        if (asp[(size_t)k * LVG_NB_ASPECT] >= opts->min_optical_depth) kept.push_back(k);
+    const int cnt = (int)kept.size();
+    *nb_out = cnt;
+    for (int j = 0; j < cnt && j < max_out; j++) {
+        const int k = kept[cnt - 1 - j], n = sel[k];   // the reference's list is push_front
+        lvg_transition &r = out[j];
+        r.up = lu[n]; r.low = ll[n];
+        r.lay_nb_hg = (int)sums[4 * (size_t)n + 3];
+        r.reserved = 0;
+        r.energy = le[n];
+        r.inv = sums[4 * (size_t)n + 0];
+        r.gain = sums[4 * (size_t)n + 1];
+        r.tau_eff = sums[4 * (size_t)n + 2];
+        r.tau_max = asp[(size_t)k * LVG_NB_ASPECT];
+        memcpy(r.tau_vs_aspect_ratio, &asp[(size_t)k * LVG_NB_ASPECT], sizeof r.tau_vs_aspect_ratio);
+        memcpy(r.tau_vs_frequency, &freq[(size_t)k * LVG_NB_FREQ], sizeof r.tau_vs_frequency);
+        const size_t off = (size_t)n * nl;
+        if (inv_arr) HIPCHECK(h, hipMemcpy(inv_arr + (size_t)j * nl, d_inv + off, sizeof(double) * nl, hipMemcpyDeviceToHost));
+        if (gain_arr) HIPCHECK(h, hipMemcpy(gain_arr + (size_t)j * nl, d_gain + off, sizeof(double) * nl, hipMemcpyDeviceToHost));
+        if (exc_temp_arr) HIPCHECK(h, hipMemcpy(exc_temp_arr + (size_t)j * nl, d_exc + off, sizeof(double) * nl, hipMemcpyDeviceToHost));
+    }
+    return LVG_OK;
+}
+

@@ -92,3 +92,29 @@ struct LvgLaunch {
     double   *dbg_matrix, *dbg_df, *dbg_pop_in;
     int       dbg_mode;               // 0 solve, 1 debug calc_new_pop, 2 boundary pops only
 };
+
+// Parameter block of the post-processing kernels (lvg_transitions.hip).
+namespace lvgtr {
+struct TrArgs {
+    int N, nb_lines, nb_lay, nb_comp, soa_ld;
+    const int *line_u, *line_l;
+    const double *line_aul, *line_e, *line_sigma;   // sigma: [comp][line]
+    const double *g;                                // [N]
+    double mass;
+    const double *soa;                              // [10 + nb_comp][soa_ld] layer SoA
+    const double *pops;                             // [nb_lay][N]
+    const double *dz, *vel_n;                       // [nb_lay]
+    double height, rel_error, velocity_shift, delta_aspect;
+    int h2o22_up, h2o22_low;
+    // per (line, layer) outputs, [nb_lines][nb_lay]
+    double *inv, *gain, *exc, *lop, *dop;
+    double *vw;                                     // [nb_lay] thermal + turbulent width
+    int *inverted;                                  // [nb_lines]
+    double *line_sum;                               // [nb_lines][4]: inv, gain, tau_eff, lay_nb_hg
+    // profile stage
+    const int *sel;                                 // [nb_sel] line indices (inverted lines)
+    int nb_sel;
+    double *od;                                     // [nb_sel][NB_FREQ][NB_ASPECT]
+    double *tau_asp, *tau_freq;                     // [nb_sel][37], [nb_sel][300]
+};
+}  // namespace lvgtr

@@ -19,7 +19,8 @@ LIB_PATH = os.environ.get("LVG_LIB_PATH") or os.path.join(_PKG, "_lib", "liblvg_
 # every symbol include/lvg_amd.h declares
 EXPORTS = ("lvg_abi_version", "lvg_solve_opts_default", "lvg_create", "lvg_destroy", "lvg_last_error",
            "lvg_nb_lev", "lvg_solve_layers", "lvg_layer_soa_rows", "lvg_solve_layers_device",
-           "lvg_debug_calc_new_pop", "lvg_boundary_layer_populations", "lvg_last_kernel_time")
+           "lvg_debug_calc_new_pop", "lvg_boundary_layer_populations", "lvg_find_opts_default",
+           "lvg_find_transitions", "lvg_last_kernel_time")
 
 _lib = None
 
@@ -50,6 +51,8 @@ def load(path: str = LIB_PATH):
     L.lvg_debug_calc_new_pop.argtypes = [vp, vp, i, dp, i, dp, dp, dp, dp]
     L.lvg_boundary_layer_populations.argtypes = [vp, vp, dp]
     L.lvg_last_kernel_time.argtypes = [vp, dp, C.POINTER(C.c_int)]
+    L.lvg_find_opts_default.argtypes = [vp]
+    L.lvg_find_transitions.argtypes = [vp, vp, vp, dp, vp, i, C.POINTER(C.c_int), vp, dp, dp, dp]
     _lib = L
     return L
 
@@ -130,3 +133,26 @@ class LvgSolver:
         self._check(self.lib.lvg_boundary_layer_populations(self.h, cl.ptr, abi.dptr(out)),
                     "lvg_boundary_layer_populations")
         return out
+
+    def find_transitions(self, layers: abi.Layers, geo: "abi.Geometry", pops, opts=None, max_out: int = 256):
+        """transition_data_container::find on the device -> (records, inv, gain, exc_temp):
+        records is a TRANSITION_DTYPE array in the reference's list order, the per-layer
+        arrays are [n, nb_lay]."""
+        o = opts if opts is not None else abi.find_opts()
+        cl = layers.to_c()
+        cg = geo.to_c()
+        p = np.ascontiguousarray(pops, dtype=np.float64)
+        nl = layers.nb_lay
+        while True:
+            out = np.zeros(max_out, dtype=abi.TRANSITION_DTYPE)
+            inv = np.zeros((max_out, nl)); gain = np.zeros((max_out, nl)); exc = np.zeros((max_out, nl))
+            n = C.c_int()
+            rc = self.lib.lvg_find_transitions(self.h, cl.ptr, C.byref(cg), abi.dptr(p), C.byref(o), max_out,
+                                               C.byref(n), out.ctypes.data_as(C.c_void_p), abi.dptr(inv),
+                                               abi.dptr(gain), abi.dptr(exc))
+            self._check(rc, "lvg_find_transitions")
+            if n.value <= max_out:
+                k = n.value
+                return out[:k].copy(), inv[:k].copy(), gain[:k].copy(), exc[:k].copy()
+            max_out = n.value
+

@@ -281,3 +281,15 @@ def make_problem(name: str, nb_lay: int | None = None, nb_lev: int | None = None
         layers = random_layers(lrng, L, (20, 200), (1e4, 1e8), (1e-8, 1e-5), (1e-10, 1e-7))
     prob = Problem(mol=mol, coll=coll, dust=dust, esc=esc, overlap1=ov1, overlap2=ov2)
     return prob, layers, opts
+
+
+def geometry(nb_lay: int, seed: int = 7, v_shock: float = 2.0e6, dz: float = 1.0e13):
+    """Synthetic cloud geometry for the post-processing (synth_v1): layer thickness
+    dz (cm, +-20 %), gas velocity decreasing from v_shock to 0 across the layers as in
+    a C-shock profile (cm/s); height = zu(last) - zl(first) = sum of dz."""
+    from .abi import Geometry
+    rng = np.random.default_rng(seed)
+    d = dz * rng.uniform(0.8, 1.2, nb_lay)
+    vel = v_shock * (1. - np.linspace(0., 1., nb_lay)) ** 2
+    return Geometry(d, vel, float(d.sum()))
+
