@@ -285,6 +285,21 @@ int         lvg_find_transitions(lvg_handle *h, const lvg_layers *layers, const 
                                  const double *pops, const lvg_find_opts *opts, int max_out, int *nb_out,
                                  lvg_transition *out, double *inv_arr, double *gain_arr, double *exc_temp_arr);
 
+/* lim_luminosity_lvg (maser_luminosity.cpp:7-106) for the transitions (up[t], low[t])
+ * (e.g. those lvg_find_transitions kept), on the device. Per transition and layer:
+ * the loss rates of both levels (radiative terms through intensity_calc, then the
+ * neutral collision rates to every other level, in level order), the limiting
+ * luminosity, pump efficiency, loss rate, pump rate and emission measure; lum[t] is
+ * the dz-weighted cloud average. The reference passes the FIRST layer's populations
+ * to intensity_calc (level_pop, :54, :58); layer_pops_in_intensity = 0 reproduces
+ * that, 1 uses each layer's own populations. Per-layer outputs: host
+ * [nb_trans*nb_lay] or NULL. */
+int         lvg_lim_luminosity(lvg_handle *h, const lvg_layers *layers, const lvg_cloud_geometry *geo,
+                               const double *pops, int nb_trans, const int *up, const int *low,
+                               int layer_pops_in_intensity, double *lum, double *lum_arr,
+                               double *emiss_coeff_arr, double *pump_rate_arr, double *pump_eff_arr,
+                               double *loss_rate_arr);
+
 /* Kernel timing of the last lvg_solve_layers* call on this handle, measured
  * with HIP events on the stream the kernels ran on: total milliseconds of the
  * solve kernel(s) and their count. */

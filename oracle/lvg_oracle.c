@@ -1146,5 +1146,77 @@ int oracle_find_transitions(const lvg_problem *P, const lvg_layers *L, const lvg
     return 0;
 }
 
+/* lim_luminosity_lvg (maser_luminosity.cpp:7-106). intensity_calc gets the FIRST
+ * layer's populations (level_pop, :54, :58) unless layer_pops != 0. */
+int oracle_lim_luminosity(const lvg_problem *P, const lvg_layers *L, const lvg_cloud_geometry *G, const double *pops,
+                          int nb_trans, const int *up, const int *low, int layer_pops, double *lum, double *lum_arr,
+                          double *emiss_coeff_arr, double *pump_rate_arr, double *pump_eff_arr, double *loss_rate_arr)
+{
+    const int N = P->mol->nb_lev, nlay = L->nb_lay;
+    const double *A = P->mol->einst;
+    const int *g = P->mol->g;
+    scheme_t S;
+    if (scheme_init(&S, P, 0)) return -1;
+    double *up_loss = (double *)calloc((size_t)nlay * 2, sizeof(double)), *low_loss = up_loss + nlay;
+    for (int t = 0; t < nb_trans; t++) {
+        const int lo = low[t], hi = up[t];
+        double lsum = 0.;
+        for (int lay = 0; lay < nlay; lay++) {
+            const int shift = N * lay;
+            const double *ipop = layer_pops ? pops + shift : pops;
+            scheme_set_layer(&S, L, lay);
+            for (int k = 0; k <= 1; k++) {
+                const int j = k == 0 ? lo : hi;
+                double loss_rate = 0.;
+                for (int i = 0; i < N; i++) {
+                    if (A[i * N + j] != 0 && i != lo && i != hi) {
+                        if (i < j && pops[shift + i] * A[i * N + j] > pops[shift + j] * A[j * N + i]) {
+                            double intensity = intensity_single(&S, j, i, ipop);
+                            loss_rate += A[j * N + i] * (1. + intensity);
+                        } else if (i > j && pops[shift + i] * A[i * N + j] < pops[shift + j] * A[j * N + i]) {
+                            double intensity = intensity_single(&S, i, j, ipop);
+                            loss_rate += A[j * N + i] * intensity;
+                        }
+                    }
+                }
+                if (k == 0) low_loss[lay] = loss_rate; else up_loss[lay] = loss_rate;
+            }
+            /* collisional_transitions::get_rate_neutrals(init, fin) (coll_rates.cpp:225-240) */
+            for (int i = 0; i < N; i++) {
+                double d, u;
+                if (i != lo) {
+                    if (lo > i) { get_rate_neutrals(&S, lo, i, &d, &u); low_loss[lay] += d; }
+                    else        { get_rate_neutrals(&S, i, lo, &d, &u); low_loss[lay] += u; }
+                }
+                if (i != hi) {
+                    if (hi > i) { get_rate_neutrals(&S, hi, i, &d, &u); up_loss[lay] += d; }
+                    else        { get_rate_neutrals(&S, i, hi, &d, &u); up_loss[lay] += u; }
+                }
+            }
+            const size_t o = (size_t)t * nlay + lay;
+            const double ph2 = L->ph2_conc[lay], oh2 = L->oh2_conc[lay], mol = L->mol_conc[lay];
+            if (emiss_coeff_arr) emiss_coeff_arr[o] = (ph2 + oh2) * mol / L->vel_grad[lay];
+            const double inversion = pops[shift + hi] / g[hi] - pops[shift + lo] / g[lo];
+            double la, pe;
+            if (inversion > 0.) {
+                la = inversion / (1. / (up_loss[lay] * g[hi]) + 1. / (low_loss[lay] * g[lo])) * mol;
+                pe = inversion / (pops[shift + hi] / g[hi] + pops[shift + lo] / g[lo]);
+            } else {
+                la = pe = 1.e-99;
+            }
+            if (lum_arr) lum_arr[o] = la;
+            if (pump_eff_arr) pump_eff_arr[o] = pe;
+            lsum += la * G->dz[lay];
+            if (loss_rate_arr) loss_rate_arr[o] = (up_loss[lay] * g[hi] + low_loss[lay] * g[lo]) / ((double)g[hi] + g[lo]);
+            if (pump_rate_arr)
+                pump_rate_arr[o] = 0.5 * (pops[shift + hi] * up_loss[lay] + pops[shift + lo] * low_loss[lay]) / (ph2 + oh2);
+        }
+        if (lum) lum[t] = lsum / G->height;
+    }
+    free(up_loss);
+    scheme_free(&S);
+    return 0;
+}
+
 double oracle_exp(double x) { return lvg_exp(x); }
 double oracle_log10(double x) { return lvg_log10(x); }

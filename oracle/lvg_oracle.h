@@ -29,6 +29,9 @@ void   oracle_find_opts_default(lvg_find_opts *o);
 int    oracle_find_transitions(const lvg_problem *P, const lvg_layers *L, const lvg_cloud_geometry *G,
                                const double *pops, const lvg_find_opts *o, int max_out, int *nb_out,
                                lvg_transition *out, double *inv_arr, double *gain_arr, double *exc_temp_arr);
+int    oracle_lim_luminosity(const lvg_problem *P, const lvg_layers *L, const lvg_cloud_geometry *G, const double *pops,
+                             int nb_trans, const int *up, const int *low, int layer_pops, double *lum, double *lum_arr,
+                             double *emiss_coeff_arr, double *pump_rate_arr, double *pump_eff_arr, double *loss_rate_arr);
 double oracle_exp(double x);
 double oracle_log10(double x);
 #ifdef __cplusplus

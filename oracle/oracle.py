@@ -55,6 +55,8 @@ def lib():
         L.oracle_dust_absorption.restype = d
         L.oracle_lu_solve.argtypes = [dp, dp, i]
         L.oracle_find_transitions.argtypes = [vp, vp, vp, dp, vp, i, C.POINTER(C.c_int), vp, dp, dp, dp]
+        ipp = C.POINTER(C.c_int)
+        L.oracle_lim_luminosity.argtypes = [vp, vp, vp, dp, i, ipp, ipp, i, dp, dp, dp, dp, dp, dp]
         L.oracle_exp.argtypes = [d]
         L.oracle_exp.restype = d
         L.oracle_log10.argtypes = [d]
@@ -150,4 +152,14 @@ def find_transitions(prob, layers, geo, pops, opts=None, max_out: int = 256):
             k = n.value
             return out[:k].copy(), inv[:k].copy(), gain[:k].copy(), exc[:k].copy()
         max_out = n.value
+
+
+def lim_luminosity(prob, layers, geo, pops, up, low, layer_pops: int = 0):
+    """oracle_lim_luminosity: same outputs as LvgSolver.lim_luminosity."""
+    from radiative_transfer_amd.native import _lim_lum_call
+    cp = prob.to_c()
+
+    def check(rc):
+        assert rc == 0
+    return _lim_lum_call(lib().oracle_lim_luminosity, check, cp.ptr, layers, geo, pops, up, low, layer_pops)
 

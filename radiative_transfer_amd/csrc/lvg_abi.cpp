@@ -28,6 +28,8 @@ extern "C" hipError_t lvg_launch_solve(const LvgDevProblem *P, const LvgLaunch *
 extern "C" hipError_t lvg_launch_debug(const LvgDevProblem *P, const LvgLaunch *L, hipStream_t s);
 extern "C" int lvg_kernel_max_levels(void);
 extern "C" hipError_t lvg_kernel_occupancy(int *blocks_per_cu);
+extern "C" hipError_t lvg_launch_lum(const LvgDevProblem *P, const LvgLaunch *L, const LvgLumArgs *A, int grid,
+                                     int nb_trans, int nb_lay, hipStream_t s);
 extern "C" hipError_t lvg_tr_launch(int stage, const void *args_dev, int nb_lines, int nb_lay, int nb_sel, hipStream_t s);
 
 namespace {
@@ -987,6 +989,58 @@ int lvg_find_transitions(lvg_handle *h, const lvg_layers *layers, const lvg_clou
         if (gain_arr) HIPCHECK(h, hipMemcpy(gain_arr + (size_t)j * nl, d_gain + off, sizeof(double) * nl, hipMemcpyDeviceToHost));
         if (exc_temp_arr) HIPCHECK(h, hipMemcpy(exc_temp_arr + (size_t)j * nl, d_exc + off, sizeof(double) * nl, hipMemcpyDeviceToHost));
     }
+    return LVG_OK;
+}
+
+int lvg_lim_luminosity(lvg_handle *h, const lvg_layers *layers, const lvg_cloud_geometry *geo, const double *pops,
+                       int nb_trans, const int *up, const int *low, int layer_pops, double *lum, double *lum_arr,
+                       double *emiss_coeff_arr, double *pump_rate_arr, double *pump_eff_arr, double *loss_rate_arr) {
+    if (!h) return LVG_E_STATE;
+    if (!layers || !geo || nb_trans < 0 || (nb_trans > 0 && (!up || !low)))
+        return fail(h, LVG_E_ARG, "lvg_lim_luminosity: missing argument");
+    const int nl = layers->nb_lay, N = h->N;
+    if (nl == 0 || nb_trans == 0) return LVG_OK;
+    if (!pops || !geo->dz) return fail(h, LVG_E_ARG, "lvg_lim_luminosity: pops / dz missing");
+    for (int t = 0; t < nb_trans; t++)
+        if (up[t] <= low[t] || low[t] < 0 || up[t] >= N) return fail(h, LVG_E_ARG, "transition %d: need N > up > low >= 0", t);
+    if (2 * nb_trans > N * N) return fail(h, LVG_E_UNSUPPORTED, "too many transitions for the slot scratch");
+    HIPCHECK(h, hipSetDevice(h->device));
+    int rc = upload_layers(h, layers);
+    if (rc) return rc;
+    if ((rc = grow(h, (void **)&h->d_pops, &h->pops_cap, sizeof(double) * (size_t)nl * N))) return rc;
+    HIPCHECK(h, hipMemcpy(h->d_pops, pops, sizeof(double) * (size_t)nl * N, hipMemcpyHostToDevice));
+    const int grid = std::max(1, std::min(nl, h->cus * h->blocks_per_cu));
+    if ((rc = ensure_workspace(h, grid))) return rc;
+    TmpDev T;
+    const size_t ntl = (size_t)nb_trans * nl;
+    int *d_up = T.alloc<int>(nb_trans), *d_low = T.alloc<int>(nb_trans);
+    double *d_dz = T.alloc<double>(nl), *d_lum = T.alloc<double>(nb_trans);
+    double *d_arr[5];
+    for (auto &p : d_arr) p = T.alloc<double>(ntl);
+    LvgLumArgs *d_args = T.alloc<LvgLumArgs>(1);
+    if (!d_up || !d_low || !d_dz || !d_lum || !d_arr[0] || !d_arr[1] || !d_arr[2] || !d_arr[3] || !d_arr[4] || !d_args)
+        return fail(h, LVG_E_NOMEM, "lvg_lim_luminosity: device allocation failed");
+    HIPCHECK(h, hipMemcpy(d_up, up, sizeof(int) * nb_trans, hipMemcpyHostToDevice));
+    HIPCHECK(h, hipMemcpy(d_low, low, sizeof(int) * nb_trans, hipMemcpyHostToDevice));
+    HIPCHECK(h, hipMemcpy(d_dz, geo->dz, sizeof(double) * nl, hipMemcpyHostToDevice));
+    LvgLumArgs a{};
+    a.nb_trans = nb_trans; a.layer_pops = layer_pops ? 1 : 0; a.up = d_up; a.low = d_low; a.dz = d_dz; a.height = geo->height;
+    a.lum = d_lum; a.lum_arr = d_arr[0]; a.emiss = d_arr[1]; a.pump_rate = d_arr[2]; a.pump_eff = d_arr[3]; a.loss_rate = d_arr[4];
+    HIPCHECK(h, hipMemcpy(d_args, &a, sizeof a, hipMemcpyHostToDevice));
+    lvg_solve_opts o;
+    lvg_solve_opts_default(&o);
+    LvgLaunch L;
+    fill_launch(h, L, &o);
+    L.nb_lay = nl; L.lay_offset = 0; L.soa_ld = nl; L.soa = h->d_soa; L.pops = h->d_pops;
+    const LvgLaunch *dL = nullptr;
+    if ((rc = push_launch(h, L, 0, h->stream, &dL))) return rc;
+    HIPCHECK(h, hipMemsetAsync(h->counter, 0, sizeof(int), h->stream));
+    HIPCHECK(h, lvg_launch_lum(h->d_prob, dL, d_args, grid, nb_trans, nl, h->stream));
+    HIPCHECK(h, hipStreamSynchronize(h->stream));
+    if (lum) HIPCHECK(h, hipMemcpy(lum, d_lum, sizeof(double) * nb_trans, hipMemcpyDeviceToHost));
+    double *outs[5] = {lum_arr, emiss_coeff_arr, pump_rate_arr, pump_eff_arr, loss_rate_arr};
+    for (int k = 0; k < 5; k++)
+        if (outs[k]) HIPCHECK(h, hipMemcpy(outs[k], d_arr[k], sizeof(double) * ntl, hipMemcpyDeviceToHost));
     return LVG_OK;
 }
 

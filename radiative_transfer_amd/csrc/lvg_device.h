@@ -93,6 +93,15 @@ struct LvgLaunch {
     int       dbg_mode;               // 0 solve, 1 debug calc_new_pop, 2 boundary pops only
 };
 
+// lim_luminosity_lvg parameters (lum_kernel in lvg_kernels.hip)
+struct LvgLumArgs {
+    int nb_trans, layer_pops;          // layer_pops: 0 = intensity_calc sees layer 0 (reference)
+    const int *up, *low;               // [nb_trans]
+    const double *dz;                  // [nb_lay]
+    double height;
+    double *lum, *lum_arr, *emiss, *pump_rate, *pump_eff, *loss_rate;   // [nb_trans], [nb_trans][nb_lay]
+};
+
 // Parameter block of the post-processing kernels (lvg_transitions.hip).
 namespace lvgtr {
 struct TrArgs {

@@ -336,7 +336,8 @@ __device__ __forceinline__ void load_rule_table(const LvgDevProblem &P, Smem &sm
 // ascending column sum, row 0 <- 1. Level pairs (f > s) are walked in 16x16 tiles
 // of the lower triangle, one pair per thread: table reads and the K[f][s] writes
 // are 128-byte row segments, every lane is busy.
-__device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P, Smem &sm, double *K, double *B) {
+__device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P, Smem &sm, double *K, double *B,
+                                                          bool electrons = true) {
     const int N = P.N, t = threadIdx.x;
     const double T = sm.T, Te = sm.Te;
     const int nt = (N + 15) >> 4, ntiles = nt * (nt + 1) / 2;
@@ -396,7 +397,7 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
             else dn = 0.;
             double dE = 0., uE = 0.;
             const int et = sm.tet[cl];
-            if (et >= 0) {
+            if (et >= 0 && electrons) {
                 const double deriv = (c1[u][LVG_MAX_TERMS] - c0[u][LVG_MAX_TERMS]) / sm.tdt[et];
                 dE = (c0[u][LVG_MAX_TERMS] + deriv * sm.tx[et]) * sm.ne;
                 if (dE > MIN_COLLISION_RATE) uE = dE * lvg_exp(de * CM_INVERSE_TO_KELVINS / Te) * P.g[f] / P.g[s];
@@ -1227,7 +1228,96 @@ __global__ void __launch_bounds__(BT, 2) debug_kernel(const LvgDevProblem *__res
     if (t == 0) Lc.dbg_df[N] = eq;
 }
 
+// lim_luminosity_lvg (maser_luminosity.cpp:7-106): one workgroup per layer (persistent
+// queue), one thread per (transition, level of it). Loss rate of level j: radiative
+// terms A_ji (1 + I) / A_ji I over the partners i without inversion (intensity_calc
+// with the first layer's populations, as the reference, or the layer's own), then the
+// neutral collision rates j -> i for every i (coll_rates.cpp:225-240) in level order,
+// read from the neutral-only collision operator K_n (rate j -> i = K_n[i][j]).
+__global__ void __launch_bounds__(BT, 2) lum_kernel(const LvgDevProblem *__restrict__ Pp,
+                                                     const LvgLaunch *__restrict__ Lp,
+                                                     const LvgLumArgs *__restrict__ Ap) {
+    __shared__ Smem sm;
+    const LvgDevProblem &P = *Pp;
+    const LvgLaunch &Lc = *Lp;
+    const LvgLumArgs &A = *Ap;
+    load_rule_table(P, sm);
+    Slot S = make_slot(P, Lc, blockIdx.x);
+    const LvgModeLines &M = P.plain;
+    const int N = P.N, t = threadIdx.x, T = A.nb_trans, nl = Lc.nb_lay;
+    const int64_t ld = Lc.soa_ld;
+    for (;;) {
+        if (t == 0) sm.layer = atomicAdd(Lc.counter, 1);
+        __syncthreads();
+        const int l = sm.layer;
+        __syncthreads();
+        if (l >= nl) break;
+        layer_setup(P, Lc, l, sm);
+        build_collision_operators(P, sm, S.K, nullptr, false);
+        const double *pl = Lc.pops + (int64_t)l * N;
+        const double *ip = A.layer_pops ? pl : Lc.pops;
+        for (int w = t; w < 2 * T; w += BT) {
+            const int tr = w >> 1, lo = A.low[tr], hi = A.up[tr], j = (w & 1) ? hi : lo;
+            double loss = 0.;
+            for (int i = 0; i < N; i++) {
+                const double aij = P.einst[i * N + j];
+                if (aij != 0. && i != lo && i != hi) {
+                    const double aji = P.einst[j * N + i];
+                    if (i < j && pl[i] * aij > pl[j] * aji) {
+                        const double I = intensity_single(P, M, sm, M.line_idx[i * N + j] >> 1, ip);
+                        loss += aji * (1. + I);
+                    } else if (i > j && pl[i] * aij < pl[j] * aji) {
+                        const double I = intensity_single(P, M, sm, M.line_idx[j * N + i] >> 1, ip);
+                        loss += aji * I;
+                    }
+                }
+            }
+            for (int i = 0; i < N; i++)
+                if (i != j) loss += S.K[i * N + j];
+            S.A[w] = loss;                   // slot scratch: [2T] loss rates (low, up)
+        }
+        __syncthreads();
+        const double *s_ = Lc.soa + l;
+        const double ph2 = s_[4 * ld], oh2 = s_[5 * ld], mol = s_[7 * ld], velg = s_[9 * ld];
+        for (int tr = t; tr < T; tr += BT) {
+            const int lo = A.low[tr], hi = A.up[tr];
+            const double low_loss = S.A[2 * tr], up_loss = S.A[2 * tr + 1];
+            const double gu = P.g[hi], gl = P.g[lo];
+            const int64_t o = (int64_t)tr * nl + l;
+            A.emiss[o] = (ph2 + oh2) * mol / velg;
+            const double inversion = pl[hi] / gu - pl[lo] / gl;
+            if (inversion > 0.) {
+                A.lum_arr[o] = inversion / (1. / (up_loss * gu) + 1. / (low_loss * gl)) * mol;
+                A.pump_eff[o] = inversion / (pl[hi] / gu + pl[lo] / gl);
+            } else {
+                A.lum_arr[o] = A.pump_eff[o] = 1.e-99;
+            }
+            A.loss_rate[o] = (up_loss * gu + low_loss * gl) / (gu + gl);
+            A.pump_rate[o] = 0.5 * (pl[hi] * up_loss + pl[lo] * low_loss) / (ph2 + oh2);
+        }
+        __syncthreads();
+    }
+}
+
+// cloud average of the luminosity, summed in layer order (one thread per transition)
+__global__ void __launch_bounds__(64) lum_reduce_kernel(const LvgLumArgs *__restrict__ Ap, int nl) {
+    const LvgLumArgs &A = *Ap;
+    const int tr = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tr >= A.nb_trans) return;
+    double s = 0.;
+    for (int l = 0; l < nl; l++) s += A.lum_arr[(int64_t)tr * nl + l] * A.dz[l];
+    A.lum[tr] = s / A.height;
+}
+
 }  // namespace lvg
+
+extern "C" hipError_t lvg_launch_lum(const LvgDevProblem *P, const LvgLaunch *L, const LvgLumArgs *A, int grid,
+                                     int nb_trans, int nb_lay, hipStream_t s) {
+    hipLaunchKernelGGL(lvg::lum_kernel, dim3(grid), dim3(lvg::BT), 0, s, P, L, A);
+    hipLaunchKernelGGL(lvg::lum_reduce_kernel, dim3((nb_trans + 63) / 64), dim3(64), 0, s, A, nb_lay);
+    (void)nb_lay;
+    return hipGetLastError();
+}
 
 // P and L are DEVICE pointers to the parameter blocks
 extern "C" hipError_t lvg_launch_solve(const LvgDevProblem *P, const LvgLaunch *L, int grid, hipStream_t s) {

@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get("LVG_LIB_PATH") or os.path.join(_PKG, "_lib", "liblvg_
 EXPORTS = ("lvg_abi_version", "lvg_solve_opts_default", "lvg_create", "lvg_destroy", "lvg_last_error",
            "lvg_nb_lev", "lvg_solve_layers", "lvg_layer_soa_rows", "lvg_solve_layers_device",
            "lvg_debug_calc_new_pop", "lvg_boundary_layer_populations", "lvg_find_opts_default",
-           "lvg_find_transitions", "lvg_last_kernel_time")
+           "lvg_find_transitions", "lvg_lim_luminosity", "lvg_last_kernel_time")
 
 _lib = None
 
@@ -52,6 +52,8 @@ def load(path: str = LIB_PATH):
     L.lvg_boundary_layer_populations.argtypes = [vp, vp, dp]
     L.lvg_last_kernel_time.argtypes = [vp, dp, C.POINTER(C.c_int)]
     L.lvg_find_opts_default.argtypes = [vp]
+    ip = C.POINTER(C.c_int)
+    L.lvg_lim_luminosity.argtypes = [vp, vp, vp, dp, i, ip, ip, i, dp, dp, dp, dp, dp, dp]
     L.lvg_find_transitions.argtypes = [vp, vp, vp, dp, vp, i, C.POINTER(C.c_int), vp, dp, dp, dp]
     _lib = L
     return L
@@ -155,4 +157,26 @@ class LvgSolver:
                 k = n.value
                 return out[:k].copy(), inv[:k].copy(), gain[:k].copy(), exc[:k].copy()
             max_out = n.value
+
+    def lim_luminosity(self, layers: abi.Layers, geo: "abi.Geometry", pops, up, low, layer_pops: int = 0):
+        """lim_luminosity_lvg on the device -> dict(lum [T], lum_arr, emiss, pump_rate, pump_eff,
+        loss_rate [T, nb_lay])."""
+        return _lim_lum_call(self.lib.lvg_lim_luminosity, lambda rc: self._check(rc, "lvg_lim_luminosity"),
+                             self.h, layers, geo, pops, up, low, layer_pops)
+
+
+def _lim_lum_call(fn, check, first, layers, geo, pops, up, low, layer_pops):
+    cl, cg = layers.to_c(), geo.to_c()
+    p = np.ascontiguousarray(pops, dtype=np.float64)
+    u = np.ascontiguousarray(up, dtype=np.int32)
+    lo = np.ascontiguousarray(low, dtype=np.int32)
+    T, nl = len(u), layers.nb_lay
+    out = {"lum": np.zeros(T)}
+    for k in ("lum_arr", "emiss", "pump_rate", "pump_eff", "loss_rate"):
+        out[k] = np.zeros((T, nl))
+    rc = fn(first, cl.ptr, C.byref(cg), abi.dptr(p), T, abi.iptr(u), abi.iptr(lo), int(layer_pops), abi.dptr(out["lum"]),
+            abi.dptr(out["lum_arr"]), abi.dptr(out["emiss"]), abi.dptr(out["pump_rate"]), abi.dptr(out["pump_eff"]),
+            abi.dptr(out["loss_rate"]))
+    check(rc)
+    return out
 

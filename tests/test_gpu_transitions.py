@@ -52,3 +52,20 @@ def test_find_transitions_h2o22_and_truncation():
     rc = s.lib.lvg_find_transitions(s.h, cl.ptr, C.byref(cg), abi.dptr(p), C.byref(abi.find_opts()), 2, C.byref(n),
                                     out.ctypes.data_as(C.c_void_p), None, None, None)
     assert rc == 0 and n.value == len(rec) and out.tobytes() == rec[:2].tobytes()
+
+
+@pytest.mark.parametrize("name,nl,dz", [("ph2o45_1024", 1024, 1e13), ("ch3oha256_4096", 128, 3e15)])
+@pytest.mark.parametrize("layer_pops", [0, 1])
+def test_lim_luminosity_bit_exact(name, nl, dz, layer_pops):
+    """lim_luminosity_lvg (maser_luminosity.cpp:7-106) device vs oracle, both intensity modes."""
+    P, L, o = synth.make_problem(name, nb_lay=nl)
+    s = LvgSolver(P)
+    pops, _ = s.solve_layers(L, abi.default_opts(**o))
+    geo = synth.geometry(nl, dz=dz)
+    rec, *_ = s.find_transitions(L, geo, pops, abi.find_opts(min_optical_depth=0.0))
+    assert len(rec) > 0
+    up, low = rec["up"].astype(np.int32), rec["low"].astype(np.int32)
+    dev = s.lim_luminosity(L, geo, pops, up, low, layer_pops)
+    ref = oracle.lim_luminosity(P, L, geo, pops, up, low, layer_pops)
+    for k in ref:
+        assert np.array_equal(dev[k], ref[k]), k
