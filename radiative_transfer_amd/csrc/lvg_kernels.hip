@@ -577,8 +577,8 @@ struct LuSrc {
 // A: N x N row-major (physical rows) in the slot workspace, read once per block
 // column and overwritten in place by the factors (L below the pivots, U in the
 // pivot rows), never row-swapped: pivoting is virtual (perm/pos in LDS).
-// Block columns of WB = 64 columns live in registers, an 8x8 fp64 tile per thread
-// (rows 8*rg.., cols 8*cg..). For each 16-wide chunk kk to the left (earlier block
+// Block columns of WB = 32 columns live in registers, an 8x4 fp64 tile per thread
+// (tile rows 8*rg.., cols 4*cg..; tile row r = physical row perm[r] at the block load). For each 16-wide chunk kk to the left (earlier block
 // columns, then the block's own chunks once factored): the chunk's pivot rows are
 // solved against L11 (TRSM -> U rows, stored to A), then every row below is updated
 // with the chunk's L (staged transposed in LDS) and those U rows. Chunks are
@@ -660,14 +660,22 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
         TSTAMP(tp0);
         const int wJ = min(WB, N - c0);
         double acc[8][TC];
+        // The block column is held in LOGICAL row order as of this load: tile row r is
+        // physical row perm[r]. Rows below an earlier block's chunk kk are then the
+        // contiguous tile rows >= kk + 16, so whole threads and waves drop out of the
+        // updates as kk grows (virtual pivoting alone scatters them).
+        int prow[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) prow[i] = (8 * rg + i < N) ? sm.perm[8 * rg + i] : 0;
+        const int trow = (t < N) ? sm.perm[t] : 0;   // physical row of tile row t (L staging)
         // ---- block column c0..c0+wJ-1 into registers (physical rows, coalesced)
         if (!FUSED) {
 #pragma unroll
             for (int i = 0; i < 8; i++)
 #pragma unroll
                 for (int j = 0; j < TC; j++) {
-                    const int pr = 8 * rg + i, col = TC * cg + j;
-                    acc[i][j] = (pr < N && col < wJ) ? A[(int64_t)pr * N + c0 + col] : 0.;
+                    const int col = TC * cg + j;
+                    acc[i][j] = (8 * rg + i < N && col < wJ) ? A[(int64_t)prow[i] * N + c0 + col] : 0.;
                 }
         } else {
             int li[8][TC];
@@ -675,9 +683,9 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             for (int i = 0; i < 8; i++)
 #pragma unroll
                 for (int j = 0; j < TC; j++) {
-                    const int pr = 8 * rg + i, col = TC * cg + j;
-                    const bool ok = pr < N && col < wJ;
-                    const int64_t o = (int64_t)pr * N + c0 + col;
+                    const int col = TC * cg + j;
+                    const bool ok = 8 * rg + i < N && col < wJ;
+                    const int64_t o = (int64_t)prow[i] * N + c0 + col;
                     acc[i][j] = ok ? src.K[o] : 0.;
                     li[i][j] = ok ? src.li[o] : -1;
                 }
@@ -685,13 +693,13 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             for (int i = 0; i < 8; i++)
 #pragma unroll
                 for (int j = 0; j < TC; j++) {
-                    const int pr = 8 * rg + i, d = c0 + TC * cg + j;
+                    const int pr = prow[i], d = c0 + TC * cg + j;
                     double v = acc[i][j];
                     if (li[i][j] >= 0) v = v + src.y[li[i][j]];
                     if (pr == d) v = sm.diag[d < NMAX ? d : 0];
                     if (pr == 0) v = 1.;
                     acc[i][j] = v;
-                    if (src.dump && pr < N && TC * cg + j < wJ) src.dump[(int64_t)pr * N + d] = v;
+                    if (src.dump && 8 * rg + i < N && TC * cg + j < wJ) src.dump[(int64_t)pr * N + d] = v;
                 }
             // residual rows: 16 columns at a time through LDS, each thread its own row
             for (int h = 0; h < wJ; h += NB) {
@@ -700,7 +708,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
 #pragma unroll
                     for (int i = 0; i < 8; i++)
 #pragma unroll
-                        for (int j = 0; j < TC; j++) sm.pu.P[8 * rg + i][TC * g + j] = acc[i][j];
+                        for (int j = 0; j < TC; j++) sm.pu.P[prow[i]][TC * g + j] = acc[i][j];
                 }
                 __syncthreads();
                 const int nc = min(NB, wJ - h);
@@ -716,8 +724,8 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
         bool have_next = false;
         auto fetch_l = [&](int k2, double (&lr)[NB], double &l11) {
             const int nb2 = min(NB, N - k2);
-            const bool la = t < N && sm.pos[t] >= k2 + nb2;
-            const double *src_l = A + (int64_t)(la ? t : 0) * N + k2;
+            const bool la = t < N && sm.pos[trow] >= k2 + nb2;
+            const double *src_l = A + (int64_t)(la ? trow : 0) * N + k2;
 #pragma unroll
             for (int m = 0; m < NB; m++) lr[m] = (la && m < nb2) ? src_l[m] : 0.;
             const int r = t / NB, m = t - r * NB;
@@ -732,10 +740,9 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                 const int g = cg - (kk - c0) / TC;     // this thread's column group within the chunk
 #pragma unroll
                 for (int i = 0; i < 8; i++) {
-                    const int pr = 8 * rg + i;
-                    if (pr < N && g >= 0 && g < NB / TC) {
+                    if (8 * rg + i < N && g >= 0 && g < NB / TC) {
 #pragma unroll
-                        for (int j = 0; j < TC; j++) sm.pu.P[pr][TC * g + j] = acc[i][j];
+                        for (int j = 0; j < TC; j++) sm.pu.P[prow[i]][TC * g + j] = acc[i][j];
                     }
                 }
                 __syncthreads();
@@ -767,17 +774,16 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                     fetch_l(kk, lrow, l11v);
                 }
             } else {
-                const bool la = t < N && sm.pos[t] >= kk + nb;
+                const bool la = t < N && sm.pos[trow] >= kk + nb;
 #pragma unroll
-                for (int m = 0; m < NB; m++) lrow[m] = (la && m < nb) ? sm.pu.P[la ? t : 0][m] : 0.;
+                for (int m = 0; m < NB; m++) lrow[m] = (la && m < nb) ? sm.pu.P[la ? trow : 0][m] : 0.;
             }
             // ---- pivot rows of chunk kk (logical kk..kk+nb-1): their current values
             //      in this block column -> Ub (owners write from registers)
 #pragma unroll
             for (int i = 0; i < 8; i++) {
-                const int pr = 8 * rg + i;
-                if (pr < N) {
-                    const int q = sm.pos[pr] - kk;
+                if (8 * rg + i < N) {
+                    const int q = sm.pos[prow[i]] - kk;
                     if (q >= 0 && q < nb) {
 #pragma unroll
                         for (int j = 0; j < TC; j++) sm.Ub[q][TC * cg + j] = acc[i][j];
@@ -836,10 +842,11 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             //      both they and the columns left of jlo are final (stored) already,
             //      so whatever lands in their registers is never read again.
             bool any = false;
+            if (kk < c0) {
+                any = 8 * rg + 7 >= kk + nb && 8 * rg < N;   // contiguous suffix of tile rows
+            } else {
 #pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const int pr = 8 * rg + i;
-                any = any || (pr < N && sm.pos[pr] >= kk + nb);
+                for (int i = 0; i < 8; i++) any = any || (8 * rg + i < N && sm.pos[prow[i]] >= kk + nb);
             }
             if (any && TC * cg + TC - 1 >= jlo) {
                 // operands of step m+1 are read from LDS while step m computes
