@@ -888,13 +888,27 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
     for (int i = t; i < N; i += BT) sm.blog[i] = b[sm.perm[i]];
     __syncthreads();
     const int nblk = (N + NB - 1) / NB;
+    // operands of block kb, loaded one block ahead so their latency hides behind the
+    // diagonal solve: the 16x16 diagonal block (one entry per thread) and the U
+    // segment U[perm[t]][k0..k0+nb) of this thread's row (rows above the block)
+    auto load_blk = [&](int kb, double &dv, double (&u)[NB]) {
+        const int k0 = kb * NB, nb = min(NB, N - k0);
+        const int r = t / NB, c = t - r * NB;
+        dv = (r < nb && c < nb) ? A[(int64_t)sm.perm[k0 + r] * N + k0 + c] : 0.;
+        const double *row = A + (int64_t)sm.perm[t < k0 ? t : 0] * N + k0;
+#pragma unroll
+        for (int m = 0; m < NB; m++) u[m] = (t < k0 && m < nb) ? row[m] : 0.;
+    };
+    double dcur, ucur[NB], dnxt = 0., unxt[NB];
+    load_blk(nblk - 1, dcur, ucur);
     for (int kb = nblk - 1; kb >= 0; kb--) {
         const int k0 = kb * NB, nb = min(NB, N - k0);
-        for (int e = t; e < nb * nb; e += BT) {
-            int r = e / nb, c = e - r * nb;
-            sm.L11[r][c] = A[(int64_t)sm.perm[k0 + r] * N + k0 + c];
+        {
+            const int r = t / NB, c = t - r * NB;
+            if (r < nb && c < nb) sm.L11[r][c] = dcur;
         }
         __syncthreads();
+        if (kb > 0) load_blk(kb - 1, dnxt, unxt);
         if (t < 64) {
             for (int m = nb - 1; m >= 0; m--) {
                 const double xm = sm.blog[k0 + m] / sm.L11[m][m];
@@ -906,18 +920,17 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             }
         }
         __syncthreads();
-        for (int i = t; i < k0; i += BT) {
-            const double *row = A + (int64_t)sm.perm[i] * N + k0;
-            double u[NB];
-#pragma unroll
-            for (int m = 0; m < NB; m++) u[m] = (m < nb) ? row[m] : 0.;
-            double s = sm.blog[i];
+        if (t < k0) {
+            double s = sm.blog[t];
 #pragma unroll
             for (int m = NB - 1; m >= 0; m--)
-                if (m < nb) s = fma(-u[m], sm.blog[k0 + m], s);
-            sm.blog[i] = s;
+                if (m < nb) s = fma(-ucur[m], sm.blog[k0 + m], s);
+            sm.blog[t] = s;
         }
         __syncthreads();
+        dcur = dnxt;
+#pragma unroll
+        for (int m = 0; m < NB; m++) ucur[m] = unxt[m];
     }
     TACC(PH_BACKSUB, tb0);
     double emax = 0.;
