@@ -910,14 +910,24 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
         __syncthreads();
         if (kb > 0) load_blk(kb - 1, dnxt, unxt);
         if (t < 64) {
-            for (int m = nb - 1; m >= 0; m--) {
-                const double xm = sm.blog[k0 + m] / sm.L11[m][m];
-                __builtin_amdgcn_wave_barrier();
-                if (t < m) sm.blog[k0 + t] = fma(-sm.L11[t][m], xm, sm.blog[k0 + t]);
-                else if (t == m) sm.blog[k0 + m] = xm;
-                __builtin_amdgcn_s_waitcnt(0xc07f);
-                __builtin_amdgcn_wave_barrier();
+            // diagonal block by wave 0 in registers: lane r < nb holds b_r and row r of the
+            // block; x_m (lane m's b_m / U_mm once final) is broadcast by DPP row_newbcast:m
+            const int r = t & 15;
+            double bt = (t < nb) ? sm.blog[k0 + t] : 0., ur[NB];
+#pragma unroll
+            for (int m = 0; m < NB; m++) ur[m] = (t < nb) ? sm.L11[r][m] : 1.;
+#define LVG_BSUB_STEP(M_)                                                                  \
+            if ((M_) < nb) {                                                               \
+                const double xm = dpp_d<0x150 + (M_), 0xf, 0xf>(bt / ur[M_]);              \
+                if (r < (M_)) bt = fma(-ur[M_], xm, bt);                                   \
+                else if (r == (M_)) bt = xm;                                               \
             }
+            LVG_BSUB_STEP(15) LVG_BSUB_STEP(14) LVG_BSUB_STEP(13) LVG_BSUB_STEP(12)
+            LVG_BSUB_STEP(11) LVG_BSUB_STEP(10) LVG_BSUB_STEP(9) LVG_BSUB_STEP(8)
+            LVG_BSUB_STEP(7) LVG_BSUB_STEP(6) LVG_BSUB_STEP(5) LVG_BSUB_STEP(4)
+            LVG_BSUB_STEP(3) LVG_BSUB_STEP(2) LVG_BSUB_STEP(1) LVG_BSUB_STEP(0)
+#undef LVG_BSUB_STEP
+            if (t < nb) sm.blog[k0 + t] = bt;
         }
         __syncthreads();
         if (t < k0) {
