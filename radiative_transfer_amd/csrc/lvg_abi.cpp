@@ -459,7 +459,7 @@ int build(lvg_handle *h, const lvg_problem *p) {
     // collision tables, T-major, restricted to the levels the molecule uses
     std::vector<int> jmax, nbl;
     std::vector<int64_t> tgo, co;
-    std::vector<double> tg, cf;
+    std::vector<double> tg, cf, cd;
     for (int t = 0; t < D.nb_tables; t++) {
         const lvg_coll_table &T = p->coll->tables[t];
         const int nl = std::min(T.nb_lev, N);
@@ -475,6 +475,14 @@ int build(lvg_handle *h, const lvg_problem *p) {
         cf.resize(base + (size_t)imax * T.jmax);
         for (int64_t i = 0; i < imax; i++)
             for (int j = 0; j < T.jmax; j++) cf[base + (size_t)j * imax + i] = T.coeff[(size_t)i * T.jmax + j];
+        // collision_data::calc_coeff_deriv (coll_rates.cpp): slope of each T interval,
+        // the same expression get_rate evaluates, so the values are identical
+        cd.resize(cf.size(), 0.);
+        for (int j = 0; j + 1 < T.jmax; j++) {
+            const double dt = T.tgrid[j + 1] - T.tgrid[j];
+            for (int64_t i = 0; i < imax; i++)
+                cd[base + (size_t)j * imax + i] = (T.coeff[(size_t)i * T.jmax + j + 1] - T.coeff[(size_t)i * T.jmax + j]) / dt;
+        }
     }
     if ((rc = upload(h, jmax.data(), jmax.size(), &D.tab_jmax))) return rc;
     if ((rc = upload(h, nbl.data(), nbl.size(), &D.tab_nb_lev))) return rc;
@@ -482,6 +490,7 @@ int build(lvg_handle *h, const lvg_problem *p) {
     if ((rc = upload(h, co.data(), co.size(), &D.tab_c_off))) return rc;
     if ((rc = upload(h, tg.data(), tg.size(), &D.tab_tgrid))) return rc;
     if ((rc = upload(h, cf.data(), cf.size(), &D.tab_coeff))) return rc;
+    if ((rc = upload(h, cd.data(), cd.size(), &D.tab_deriv))) return rc;
     std::vector<uint8_t> pc;
     if ((rc = compile_rule(h, p, pc, D.terms))) return rc;
     if ((rc = upload(h, pc.data(), pc.size(), &D.pair_class))) return rc;

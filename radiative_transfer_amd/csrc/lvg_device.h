@@ -63,6 +63,7 @@ struct LvgDevProblem {
     const int     *tab_jmax, *tab_nb_lev;
     const int64_t *tab_tg_off, *tab_c_off;
     const double  *tab_tgrid, *tab_coeff;          // T-major coeff[t][pair]
+    const double  *tab_deriv;                      // T-major slope of interval t, [t][pair]
     const uint8_t *pair_class;                     // [N(N-1)/2]
     LvgTermTable   terms;
     // LVG escape table (lvg_method_functions.cpp:74-110)

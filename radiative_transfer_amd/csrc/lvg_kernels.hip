@@ -93,6 +93,7 @@ struct Smem {
     double teff[LVG_MAX_TABLES];
     int    lo[LVG_MAX_TABLES];
     const double *tcol[LVG_MAX_TABLES];   // coefficients at T index lo (T-major row)
+    const double *tder[LVG_MAX_TABLES];   // their slopes over [lo, lo+1]
     int64_t timax[LVG_MAX_TABLES];        // pairs per T row
     double tdt[LVG_MAX_TABLES];           // tgrid[lo+1] - tgrid[lo]
     double tx[LVG_MAX_TABLES];            // min(T, tmax) - tgrid[lo]
@@ -300,20 +301,12 @@ __device__ __forceinline__ void layer_setup(const LvgDevProblem &P, const LvgLau
             const int64_t imax = (int64_t)P.tab_nb_lev[tb] * (P.tab_nb_lev[tb] - 1) / 2;
             sm.timax[tb] = imax;
             sm.tcol[tb] = P.tab_coeff + P.tab_c_off[tb] + (int64_t)lo * imax;
+            sm.tder[tb] = P.tab_deriv + P.tab_c_off[tb] + (int64_t)lo * imax;
             sm.tdt[tb] = tg[lo + 1] - tg[lo];
             sm.tx[tb] = sm.teff[tb] - tg[lo];
         }
     }
     __syncthreads();
-}
-
-// collision_data::get_rate (coll_rates.cpp:54-69), T-major table; the per-layer
-// interval data (row pointer, dT, T - tgrid[lo]) sit in LDS (layer_setup)
-__device__ __forceinline__ double table_rate(const Smem &sm, int tb, int pair) {
-    const double *c = sm.tcol[tb];
-    const double c0 = c[pair], c1 = c[sm.timax[tb] + pair];
-    const double deriv = (c1 - c0) / sm.tdt[tb];
-    return c0 + deriv * sm.tx[tb];
 }
 
 // the compiled molecule rule, copied to LDS once per launch
@@ -368,9 +361,8 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
                 const bool ld = (k < LVG_MAX_TERMS) ? alive : (pc[u] >= 0 && tb >= 0);
                 c0[u][k] = 0.; c1[u][k] = 0.;
                 if (ld) {
-                    const double *c = sm.tcol[tb] + pc[u];
-                    c0[u][k] = c[0];
-                    c1[u][k] = c[sm.timax[tb]];
+                    c0[u][k] = sm.tcol[tb][pc[u]];
+                    c1[u][k] = sm.tder[tb][pc[u]];          // slope (calc_coeff_deriv)
                 }
             }
         }
@@ -385,8 +377,7 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
             for (int k = 0; k < LVG_MAX_TERMS; k++) {
                 const int tb = sm.ttab[cl][k];
                 if (tb < 0) break;
-                const double deriv = (c1[u][k] - c0[u][k]) / sm.tdt[tb];   // collision_data::get_rate
-                const double r = (c0[u][k] + deriv * sm.tx[tb]) * sm.cc[sm.tcombo[cl][k]];
+                const double r = (c0[u][k] + c1[u][k] * sm.tx[tb]) * sm.cc[sm.tcombo[cl][k]];   // get_rate
                 if (k < grp) dn = (k == 0) ? r : dn + r;
                 else { gsum = (ng == 0) ? r : gsum + r; ng++; }
             }
@@ -398,8 +389,7 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
             double dE = 0., uE = 0.;
             const int et = sm.tet[cl];
             if (et >= 0 && electrons) {
-                const double deriv = (c1[u][LVG_MAX_TERMS] - c0[u][LVG_MAX_TERMS]) / sm.tdt[et];
-                dE = (c0[u][LVG_MAX_TERMS] + deriv * sm.tx[et]) * sm.ne;
+                dE = (c0[u][LVG_MAX_TERMS] + c1[u][LVG_MAX_TERMS] * sm.tx[et]) * sm.ne;
                 if (dE > MIN_COLLISION_RATE) uE = dE * lvg_exp(de * CM_INVERSE_TO_KELVINS / Te) * P.g[f] / P.g[s];
                 else dE = 0.;
             }
