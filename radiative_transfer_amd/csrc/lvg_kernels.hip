@@ -350,6 +350,16 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
         }
 #pragma unroll
         for (int u = 0; u < PU; u++) cls[u] = pc[u] >= 0 ? P.pair_class[pc[u]] : 0;
+        // level data of the batch, loaded before any store of it
+        double ef[PU], es[PU], gf[PU], gs[PU], af[PU];
+#pragma unroll
+        for (int u = 0; u < PU; u++) {
+            const bool ok = pc[u] >= 0;
+            const int f = ok ? fc[u] : 1, s = ok ? sc[u] : 0;
+            ef[u] = P.energy[f]; es[u] = P.energy[s];
+            gf[u] = P.g[f]; gs[u] = P.g[s];
+            af[u] = B ? P.einst[f * N + s] : 0.;
+        }
         double c0[PU][LVG_MAX_TERMS + 1], c1[PU][LVG_MAX_TERMS + 1];
 #pragma unroll
         for (int u = 0; u < PU; u++) {
@@ -382,21 +392,21 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
                 else { gsum = (ng == 0) ? r : gsum + r; ng++; }
             }
             if (ng) dn = dn + gsum;
-            const double de = P.energy[s] - P.energy[f];
+            const double de = es[u] - ef[u];
             double un = 0.;
-            if (dn > MIN_COLLISION_RATE) un = dn * lvg_exp(de * CM_INVERSE_TO_KELVINS / T) * P.g[f] / P.g[s];
+            if (dn > MIN_COLLISION_RATE) un = dn * lvg_exp(de * CM_INVERSE_TO_KELVINS / T) * gf[u] / gs[u];
             else dn = 0.;
             double dE = 0., uE = 0.;
             const int et = sm.tet[cl];
             if (et >= 0 && electrons) {
                 dE = (c0[u][LVG_MAX_TERMS] + c1[u][LVG_MAX_TERMS] * sm.tx[et]) * sm.ne;
-                if (dE > MIN_COLLISION_RATE) uE = dE * lvg_exp(de * CM_INVERSE_TO_KELVINS / Te) * P.g[f] / P.g[s];
+                if (dE > MIN_COLLISION_RATE) uE = dE * lvg_exp(de * CM_INVERSE_TO_KELVINS / Te) * gf[u] / gs[u];
                 else dE = 0.;
             }
             K[s * N + f] = dn + dE;
             K[f * N + s] = un + uE;
             if (B) {
-                B[s * N + f] = 0.5 * P.einst[f * N + s] + dn;
+                B[s * N + f] = 0.5 * af[u] + dn;
                 B[f * N + s] = un;
             }
         }
