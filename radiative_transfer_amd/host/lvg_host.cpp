@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cmath>
 #include <fstream>
+#include <iomanip>
 #include <iostream>
 #include <limits>
 #include <sstream>
@@ -317,6 +318,107 @@ std::vector<int> calc_molecular_populations(cloud_data *cloud, iteration_scheme_
     }
     if (status) *status = std::move(st);
     return bad;
+}
+
+// ---- populations on disk ----------------------------------------------------------
+std::string save_populations(const std::string &output_path, const energy_diagram *diagram, const double *arr,
+                             int nb_cloud_lay, int nb_mol_lev, bool normalized, const std::string &id) {
+    const std::string fname = output_path + diagram->mol_name + "_populations" + id + ".txt";
+    std::ofstream f(fname);
+    if (!f.is_open()) throw lvg_error(LVG_E_ARG, "save_populations: can't open " + fname);
+    f.setf(std::ios::scientific);
+    f.precision(6);
+    f << std::left << std::setw(8) << nb_mol_lev << std::setw(8) << nb_cloud_lay << std::endl;
+    f << std::setw(6) << " ";
+    for (int j = 0; j < nb_cloud_lay; j++) f << std::left << std::setw(12) << j;
+    f << std::endl;
+    for (int i = 0; i < nb_mol_lev; i++) {
+        const double w = normalized ? 1. / ((double)diagram->lev_array[i].g) : 1.;
+        f << std::left << std::setw(6) << i;
+        // the reference writes setw(12) fields, which run together for 12-character
+        // values such as 5.000000e-01; one space keeps the columns readable
+        for (int j = 0; j < nb_cloud_lay; j++) f << std::left << std::setw(12) << arr[(size_t)j * nb_mol_lev + i] * w << ' ';
+        f << std::endl;
+    }
+    return fname;
+}
+
+void read_populations(const std::string &file_name, double *arr, int nb_cloud_lay, int nb_mol_lev) {
+    std::ifstream f(file_name);
+    if (!f.is_open()) throw lvg_error(LVG_E_ARG, "read_populations: can't open " + file_name);
+    int i, j, k;
+    f >> i >> j;
+    if (i != nb_mol_lev || j != nb_cloud_lay)
+        throw lvg_error(LVG_E_ARG, "read_populations: the numbers of columns and rows are not correct in " + file_name);
+    for (j = 0; j < nb_cloud_lay; j++) f >> k;
+    for (i = 0; i < nb_mol_lev; i++) {
+        f >> k;
+        for (j = 0; j < nb_cloud_lay; j++) f >> arr[(size_t)j * nb_mol_lev + i];
+    }
+    if (!f) throw lvg_error(LVG_E_ARG, "read_populations: truncated " + file_name);
+}
+
+// ---- post-processing ------------------------------------------------------------------
+void transition_data_container::find(const double *level_pop, double rel_error) {
+    if (!scheme || !scheme->handle()) throw lvg_error(LVG_E_STATE, "transition_data_container: scheme not initialised");
+    const int nl = cloud->nb_lay;
+    if ((int)geo->dz.size() != nl || (int)geo->vel_n.size() != nl)
+        throw lvg_error(LVG_E_ARG, "transition_data_container: geometry size != nb_lay");
+    layer_pack lp(*cloud, scheme->problem().dust->nb_comp);
+    lvg_cloud_geometry g{geo->dz.data(), geo->vel_n.data(), geo->height};
+    lvg_find_opts o;
+    lvg_find_opts_default(&o);
+    o.rel_error = rel_error;
+    o.min_optical_depth = min_optical_depth;
+    o.velocity_shift = velocity_shift;
+    o.h2o22_up = h2o22_up;
+    o.h2o22_low = h2o22_low;
+    int cap = 64, n = 0;
+    std::vector<lvg_transition> out;
+    std::vector<double> inv, gain, exc;
+    for (;;) {
+        out.assign(cap, lvg_transition{});
+        inv.assign((size_t)cap * nl, 0.); gain.assign((size_t)cap * nl, 0.); exc.assign((size_t)cap * nl, 0.);
+        check(lvg_find_transitions(scheme->handle(), &lp.view, &g, level_pop, &o, cap, &n, out.data(), inv.data(),
+                                   gain.data(), exc.data()), scheme->handle(), "find");
+        if (n <= cap) break;
+        cap = n;
+    }
+    data.clear();
+    for (int k = 0; k < n; k++) {
+        transition_data t;
+        const lvg_transition &r = out[k];
+        t.up = r.up; t.low = r.low; t.lay_nb_hg = r.lay_nb_hg; t.energy = r.energy;
+        t.inv = r.inv; t.gain = r.gain; t.tau_eff = r.tau_eff; t.tau_max = r.tau_max;
+        t.inv_arr.assign(inv.begin() + (size_t)k * nl, inv.begin() + (size_t)(k + 1) * nl);
+        t.gain_arr.assign(gain.begin() + (size_t)k * nl, gain.begin() + (size_t)(k + 1) * nl);
+        t.exc_temp_arr.assign(exc.begin() + (size_t)k * nl, exc.begin() + (size_t)(k + 1) * nl);
+        t.tau_vs_aspect_ratio.assign(r.tau_vs_aspect_ratio, r.tau_vs_aspect_ratio + LVG_NB_ASPECT);
+        t.tau_vs_frequency.assign(r.tau_vs_frequency, r.tau_vs_frequency + LVG_NB_FREQ);
+        data.push_back(std::move(t));
+    }
+}
+
+void lim_luminosity_lvg(iteration_scheme_lvg *scheme, transition_data_container *c, const cloud_data *cloud,
+                        const double *level_pop, bool first_layer_pops) {
+    if (!scheme || !scheme->handle() || !c) throw lvg_error(LVG_E_STATE, "lim_luminosity_lvg: bad arguments");
+    const int nl = cloud->nb_lay, T = (int)c->data.size();
+    if (T == 0) return;
+    layer_pack lp(*cloud, scheme->problem().dust->nb_comp);
+    lvg_cloud_geometry g{c->geo->dz.data(), c->geo->vel_n.data(), c->geo->height};
+    std::vector<int> up(T), low(T);
+    for (int t = 0; t < T; t++) { up[t] = c->data[t].up; low[t] = c->data[t].low; }
+    std::vector<double> lum(T), arr[5];
+    for (auto &a : arr) a.assign((size_t)T * nl, 0.);
+    check(lvg_lim_luminosity(scheme->handle(), &lp.view, &g, level_pop, T, up.data(), low.data(),
+                             first_layer_pops ? 0 : 1, lum.data(), arr[0].data(), arr[1].data(), arr[2].data(),
+                             arr[3].data(), arr[4].data()), scheme->handle(), "lim_luminosity_lvg");
+    for (int t = 0; t < T; t++) {
+        transition_data &d = c->data[t];
+        d.lum = lum[t];
+        auto row = [&](int k) { return std::vector<double>(arr[k].begin() + (size_t)t * nl, arr[k].begin() + (size_t)(t + 1) * nl); };
+        d.lum_arr = row(0); d.emiss_coeff_arr = row(1); d.pump_rate_arr = row(2); d.pump_eff_arr = row(3); d.loss_rate_arr = row(4);
+    }
 }
 
 }  // namespace lvgamd

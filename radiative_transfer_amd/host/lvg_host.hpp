@@ -254,4 +254,51 @@ std::vector<int> calc_molecular_populations(cloud_data *cloud, iteration_scheme_
                                             init_policy init = init_policy::warm_chain,
                                             std::vector<lvg_layer_status> *status = nullptr);
 
+// ---- populations on disk (spectroscopy.cpp:1294-1368) -------------------------------
+// save_populations: "<output_path><mol_name>_populations<id>.txt", N rows x nb_lay columns
+// (scientific, 6 digits), divided by g when `normalized`; unlike the reference's setw(12)
+// fields, a space follows every value (12-character values would otherwise run
+// together and not read back). read_populations: the same
+// layout back into arr[l*N + i]; throws on a size mismatch (the reference prints).
+std::string save_populations(const std::string &output_path, const energy_diagram *diagram, const double *arr,
+                             int nb_cloud_lay, int nb_mol_lev, bool normalized, const std::string &id);
+void read_populations(const std::string &file_name, double *arr, int nb_cloud_lay, int nb_mol_lev);
+
+// ---- post-processing (transition_data.h:11-80, maser_luminosity.cpp:7-106) ----------
+struct cloud_geometry {
+    std::vector<double> dz, vel_n;   // cloud_layer::dz, ::vel_n
+    double height = 0.;              // cloud_data::get_height()
+};
+
+struct transition_data {
+    int up = 0, low = 0, lay_nb_hg = 0;
+    double energy = 0., inv = 0., gain = 0., lum = 0., tau_eff = 0., tau_max = 0.;
+    std::vector<double> inv_arr, gain_arr, exc_temp_arr;
+    std::vector<double> lum_arr, emiss_coeff_arr, pump_rate_arr, pump_eff_arr, loss_rate_arr;
+    std::vector<double> tau_vs_aspect_ratio, tau_vs_frequency;
+};
+
+class transition_data_container {
+public:
+    double min_optical_depth = 0.01, velocity_shift = 5.e+5;
+    int h2o22_up = -1, h2o22_low = -1;    // the o-H2O 22 GHz line, if any
+    std::vector<transition_data> data;    // the reference's list order
+    transition_data_container(const cloud_data *cl, const cloud_geometry *geo, iteration_scheme_lvg *scheme)
+        : cloud(cl), geo(geo), scheme(scheme) {}
+    // find(level_pop, rel_error) (transition_data.cpp:380-417) on the device
+    void find(const double *level_pop, double rel_error);
+private:
+    const cloud_data *cloud;
+    const cloud_geometry *geo;
+    iteration_scheme_lvg *scheme;
+    friend void lim_luminosity_lvg(iteration_scheme_lvg *, transition_data_container *, const cloud_data *,
+                                   const double *, bool);
+};
+
+// lim_luminosity_lvg for every transition of the container, on the device. The
+// reference passes the first layer's populations to intensity_calc; keep that with
+// first_layer_pops_in_intensity = true (default).
+void lim_luminosity_lvg(iteration_scheme_lvg *calc_scheme, transition_data_container *container,
+                        const cloud_data *cloud, const double *level_pop, bool first_layer_pops_in_intensity = true);
+
 }  // namespace lvgamd

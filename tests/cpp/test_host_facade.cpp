@@ -2,6 +2,7 @@
 // surface of radiative_transfer_amd/host/lvg_host.hpp on the GPU and checks every
 // result bit for bit against the CPU oracle fed the identical lvg_problem.
 // Exit codes: 0 all equal, 1 mismatch, 3 no usable device (lvg_create failed).
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -154,6 +155,49 @@ int main(int argc, char **argv) {
     std::printf("%-44s %s (found %d, iterations %d/%d)\n", "  status", (found == (so.converged != 0) &&
                 ctl.iter_nb == so.iterations) ? "equal" : "MISMATCH", (int)found, ctl.iter_nb, so.iterations);
     failures += !(found == (so.converged != 0) && ctl.iter_nb == so.iterations);
+    // 3. populations on disk (spectroscopy.cpp:1294-1368): 6 significant digits
+    {
+        std::vector<double> pg((size_t)cloud.nb_lay * N, 0.), back((size_t)cloud.nb_lay * N, 0.);
+        calc_molecular_populations(&cloud, &scheme, &di, &ei, &co, pg.data(), N, true, 0, init_policy::boundary_layer);
+        const std::string f = save_populations(tmp, &di, pg.data(), cloud.nb_lay, N, false, "_test");
+        read_populations(f, back.data(), cloud.nb_lay, N);
+        double worst = 0.;
+        for (size_t i = 0; i < pg.size(); i++) worst = std::max(worst, std::fabs(back[i] - pg[i]) / std::fabs(pg[i]));
+        std::printf("%-44s %s (max rel %.1e)\n", "save_populations / read_populations", worst < 5e-6 ? "equal" : "MISMATCH", worst);
+        failures += !(worst < 5e-6);
+        // 4. transition_data_container::find and lim_luminosity_lvg vs the oracle
+        cloud_geometry geo;
+        for (int l = 0; l < cloud.nb_lay; l++) { geo.dz.push_back(3e16); geo.vel_n.push_back(2e6 * (1. - l / 6.)); }
+        geo.height = 3e16 * cloud.nb_lay;
+        transition_data_container tc(&cloud, &geo, &scheme);
+        tc.min_optical_depth = 0.;
+        tc.find(pg.data(), 0.);
+        lim_luminosity_lvg(&scheme, &tc, &cloud, pg.data());
+        lvg_cloud_geometry g{geo.dz.data(), geo.vel_n.data(), geo.height};
+        lvg_find_opts fo;
+        oracle_find_opts_default(&fo);
+        fo.rel_error = 0.; fo.min_optical_depth = 0.;
+        std::vector<lvg_transition> ro(256);
+        int nro = 0;
+        oracle_find_transitions(&P, &lp.view, &g, pg.data(), &fo, 256, &nro, ro.data(), nullptr, nullptr, nullptr);
+        int bad = nro != (int)tc.data.size();
+        std::vector<int> up, low;
+        for (int k = 0; !bad && k < nro; k++) {
+            bad += ro[k].up != tc.data[k].up || ro[k].low != tc.data[k].low ||
+                   std::memcmp(&ro[k].tau_max, &tc.data[k].tau_max, sizeof(double)) != 0;
+            up.push_back(ro[k].up); low.push_back(ro[k].low);
+        }
+        std::printf("%-44s %s (%d transitions)\n", "transition_data_container::find", bad ? "MISMATCH" : "equal", nro);
+        failures += bad != 0;
+        if (!bad && nro > 0) {
+            std::vector<double> lum(nro);
+            oracle_lim_luminosity(&P, &lp.view, &g, pg.data(), nro, up.data(), low.data(), 0, lum.data(), nullptr,
+                                  nullptr, nullptr, nullptr, nullptr);
+            std::vector<double> lg(nro);
+            for (int k = 0; k < nro; k++) lg[k] = tc.data[k].lum;
+            expect_equal("lim_luminosity_lvg (lum)", lg.data(), lum.data(), nro);
+        }
+    }
     std::printf(failures ? "FAILED\n" : "ALL EQUAL\n");
     return failures ? 1 : 0;
 }
