@@ -79,7 +79,7 @@ struct Smem {
     int    pos[NMAX];           // its inverse: physical row -> logical position
     double red[8];
     int    ired[8];
-    double cand[2][NW][NB];     // panel: each wave's pivot candidate row, double buffered
+    double cand[2][NW][NB + 1]; // panel: each wave's pivot candidate row and its b, double buffered
     int    candp[2][NW];        // its physical row
     double L11[NB][NB + 1];
     double Ub[NB][WB + 2];      // U rows of one chunk across the block column
@@ -591,13 +591,17 @@ struct LuSrc {
 // ------------------------------------------------------------------------------
 __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, double *b, Smem &sm) {
     // chunk columns kk..kk+nb-1 are in sm.pu.P[p][0..nb) for every physical row p;
-    // rows with pos[p] >= kk take part. One row per thread (N <= NMAX = BT).
+    // rows with pos[p] >= kk take part. One row per thread (N <= NMAX = BT), the row's
+    // right-hand side b[p] in a register; the pivot candidate of each wave publishes
+    // its row and its b through LDS.
     const int t = threadIdx.x, w = t >> 6;
     double rw[NB];
     const bool valid = t < N;
     const int p = valid ? t : 0;
-    bool act = valid && sm.pos[p] >= kk;
+    const bool part = valid && sm.pos[p] >= kk;
+    bool act = part;
     int lp = act ? sm.pos[p] - kk : 0x7fffffff;
+    double rb = b[p];
 #pragma unroll
     for (int j = 0; j < NB; j++) rw[j] = sm.pu.P[p][j];
 #pragma clang loop unroll(full)
@@ -611,21 +615,27 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
             if (act && lp == wmin) {               // this wave's candidate publishes its row
 #pragma unroll
                 for (int j = 0; j < NB; j++) if (j >= c) sm.cand[buf][w][j] = rw[j];
-                sm.candp[buf][w] = p;
+                sm.cand[buf][w][NB] = rb;
             }
             __syncthreads();                       // one barrier per column
-            double vmax = sm.red[4 * buf];
-            int lmin = sm.ired[4 * buf], ww = 0;
+            // the four candidates at once, winner picked without branches
+            double ov[NW];
+            int oi[NW];
+#pragma unroll
+            for (int i = 0; i < NW; i++) { ov[i] = sm.red[4 * buf + i]; oi[i] = sm.ired[4 * buf + i]; }
+            double vmax = ov[0];
+            int lmin = oi[0], ww = 0;
 #pragma unroll
             for (int i = 1; i < NW; i++) {
-                const double ov = sm.red[4 * buf + i];
-                const int oi = sm.ired[4 * buf + i];
-                if (ov > vmax || (ov == vmax && oi < lmin)) { vmax = ov; lmin = oi; ww = i; }
+                const bool better = ov[i] > vmax || (ov[i] == vmax && oi[i] < lmin);
+                vmax = better ? ov[i] : vmax;
+                lmin = better ? oi[i] : lmin;
+                ww = better ? i : ww;
             }
             const bool owner = act && lp == lmin;
             const double *prow = sm.cand[buf][ww];
             const double piv = prow[c];
-            const double bc = b[sm.candp[buf][ww]];
+            const double bc = prow[NB];
             if (owner) { act = false; lp = c; }
             else if (lp == c) lp = lmin;
             if (act) {
@@ -633,17 +643,18 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
                 rw[c] = l;
 #pragma unroll
                 for (int j = 0; j < NB; j++) if (j > c) rw[j] = fma(-l, prow[j], rw[j]);
-                b[p] = fma(-l, bc, b[p]);
+                rb = fma(-l, bc, rb);
             }
         }
     }
     __syncthreads();
-    if (valid && sm.pos[p] >= kk) {
+    if (part) {
         // rows of this chunk and below: factors back to A (physical row p)
 #pragma unroll
         for (int j = 0; j < NB; j++) if (j < nb) A[(int64_t)p * N + kk + j] = rw[j];
         sm.perm[kk + lp] = p;
         sm.pos[p] = kk + lp;
+        b[p] = rb;
 #pragma unroll
         for (int j = 0; j < NB; j++) sm.pu.P[p][j] = rw[j];
     }
