@@ -79,6 +79,7 @@ struct Smem {
     int    pos[NMAX];           // its inverse: physical row -> logical position
     double red[8];
     int    ired[8];
+    unsigned long long pkey[8];   // panel: per-wave pivot keys (|v| bits, active flag), double buffered
     double cand[2][NW][NB + 1]; // panel: each wave's pivot candidate row and its b, double buffered
     int    candp[2][NW];        // its physical row
     double L11[NB][NB + 1];
@@ -127,6 +128,22 @@ template <int CTRL, int ROW, int BANK>
 __device__ __forceinline__ int dpp_i(int x) {
     return __builtin_amdgcn_update_dpp(x, x, CTRL, ROW, BANK, false);
 }
+template <int CTRL, int ROW, int BANK>
+__device__ __forceinline__ unsigned dpp_u0(unsigned x) {   // out-of-row lanes read 0 (bound_ctrl)
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROW, BANK, true);
+}
+// wave-wide unsigned max; each step folds into one v_max_u32_dpp
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
+    v = max(v, dpp_u0<0x111, 0xf, 0xf>(v));   // row_shr:1
+    v = max(v, dpp_u0<0x112, 0xf, 0xf>(v));   // row_shr:2
+    v = max(v, dpp_u0<0x113, 0xf, 0xf>(v));   // row_shr:3
+    v = max(v, dpp_u0<0x114, 0xf, 0xe>(v));   // row_shr:4
+    v = max(v, dpp_u0<0x118, 0xf, 0xc>(v));   // row_shr:8
+    v = max(v, dpp_u0<0x142, 0xa, 0xf>(v));   // row_bcast:15
+    v = max(v, dpp_u0<0x143, 0xc, 0xf>(v));   // row_bcast:31
+    return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 __device__ __forceinline__ double wave_max_dpp(double v) {
     v = fmax(v, dpp_d<0x111, 0xf, 0xf>(v));   // row_shr:1
     v = fmax(v, dpp_d<0x112, 0xf, 0xf>(v));   // row_shr:2
@@ -608,10 +625,19 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
     for (int c = 0; c < NB; c++) {
         if (c < nb) {
             const int buf = c & 1;
-            const double v = act ? fabs(rw[c]) : -1.;
-            const double wmax = wave_max_dpp(v);
-            const int wmin = wave_min_dpp((v == wmax && act) ? lp : 0x7fffffff);
-            if ((t & 63) == 0) { sm.red[4 * buf + w] = wmax; sm.ired[4 * buf + w] = wmin; }
+            // argmax |v| (ties: smallest logical position) as three u32 max reductions:
+            // |v| >= 0 orders like its bit pattern; active rows carry the top bit
+            const double av = fabs(rw[c]);
+            const unsigned long long bits = (act && av == av) ? (unsigned long long)__double_as_longlong(av) : 0ull;
+            const unsigned hi = act ? ((unsigned)(bits >> 32) | 0x80000000u) : 0u, lo = (unsigned)bits;
+            const unsigned H = wave_max_u32(hi);
+            const unsigned Lw = wave_max_u32(hi == H ? lo : 0u);
+            const unsigned X = wave_max_u32((hi == H && lo == Lw && act) ? ~(unsigned)lp : 0u);
+            const int wmin = (int)~X;
+            if ((t & 63) == 0) {
+                sm.pkey[4 * buf + w] = ((unsigned long long)H << 32) | Lw;
+                sm.ired[4 * buf + w] = wmin;
+            }
             if (act && lp == wmin) {               // this wave's candidate publishes its row
 #pragma unroll
                 for (int j = 0; j < NB; j++) if (j >= c) sm.cand[buf][w][j] = rw[j];
@@ -619,16 +645,16 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
             }
             __syncthreads();                       // one barrier per column
             // the four candidates at once, winner picked without branches
-            double ov[NW];
+            unsigned long long ok[NW];
             int oi[NW];
 #pragma unroll
-            for (int i = 0; i < NW; i++) { ov[i] = sm.red[4 * buf + i]; oi[i] = sm.ired[4 * buf + i]; }
-            double vmax = ov[0];
+            for (int i = 0; i < NW; i++) { ok[i] = sm.pkey[4 * buf + i]; oi[i] = sm.ired[4 * buf + i]; }
+            unsigned long long kmax = ok[0];
             int lmin = oi[0], ww = 0;
 #pragma unroll
             for (int i = 1; i < NW; i++) {
-                const bool better = ov[i] > vmax || (ov[i] == vmax && oi[i] < lmin);
-                vmax = better ? ov[i] : vmax;
+                const bool better = ok[i] > kmax || (ok[i] == kmax && (unsigned)oi[i] < (unsigned)lmin);
+                kmax = better ? ok[i] : kmax;
                 lmin = better ? oi[i] : lmin;
                 ww = better ? i : ww;
             }
