@@ -763,8 +763,19 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             const int nb2 = min(NB, N - k2);
             const bool la = t < N && sm.pos[trow] >= k2 + nb2;
             const double *src_l = A + (int64_t)(la ? trow : 0) * N + k2;
+            if ((N & 1) == 0 && nb2 == NB) {
+                // 16-byte aligned row segment (N even, k2 a multiple of 16): 8 vector loads
+                const double2 *s2 = reinterpret_cast<const double2 *>(src_l);
 #pragma unroll
-            for (int m = 0; m < NB; m++) lr[m] = (la && m < nb2) ? src_l[m] : 0.;
+                for (int m = 0; m < NB / 2; m++) {
+                    const double2 v = la ? s2[m] : make_double2(0., 0.);
+                    lr[2 * m] = v.x;
+                    lr[2 * m + 1] = v.y;
+                }
+            } else {
+#pragma unroll
+                for (int m = 0; m < NB; m++) lr[m] = (la && m < nb2) ? src_l[m] : 0.;
+            }
             const int r = t / NB, m = t - r * NB;
             l11 = (t < NB * NB && r < nb2 && m < r) ? A[(int64_t)sm.perm[k2 + r] * N + k2 + m] : 0.;
         };
