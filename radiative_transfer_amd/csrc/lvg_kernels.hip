@@ -677,7 +677,12 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
     if (part) {
         // rows of this chunk and below: factors back to A (physical row p)
 #pragma unroll
-        for (int j = 0; j < NB; j++) if (j < nb) A[(int64_t)p * N + kk + j] = rw[j];
+        for (int j = 0; j < NB; j++) if (j < nb && !((N & 1) == 0 && nb == NB)) A[(int64_t)p * N + kk + j] = rw[j];
+        if ((N & 1) == 0 && nb == NB) {
+            double2 *d2 = reinterpret_cast<double2 *>(A + (int64_t)p * N + kk);
+#pragma unroll
+            for (int j = 0; j < NB / 2; j++) d2[j] = make_double2(rw[2 * j], rw[2 * j + 1]);
+        }
         sm.perm[kk + lp] = p;
         sm.pos[p] = kk + lp;
         b[p] = rb;
@@ -716,16 +721,31 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                 }
         } else {
             int li[8][TC];
+            static_assert(TC == 4, "vector block load assumes 4 columns per thread");
+            if ((N & 3) == 0 && TC * cg + TC <= wJ) {
+                // whole 4-column segments, 32-byte aligned: 2 x 16-byte K loads, 1 x 16-byte li load
 #pragma unroll
-            for (int i = 0; i < 8; i++)
-#pragma unroll
-                for (int j = 0; j < TC; j++) {
-                    const int col = TC * cg + j;
-                    const bool ok = 8 * rg + i < N && col < wJ;
-                    const int64_t o = (int64_t)prow[i] * N + c0 + col;
-                    acc[i][j] = ok ? src.K[o] : 0.;
-                    li[i][j] = ok ? src.li[o] : -1;
+                for (int i = 0; i < 8; i++) {
+                    const bool ok = 8 * rg + i < N;
+                    const int64_t o = (int64_t)(ok ? prow[i] : 0) * N + c0 + TC * cg;
+                    const double2 k0 = ok ? reinterpret_cast<const double2 *>(src.K + o)[0] : make_double2(0., 0.);
+                    const double2 k1 = ok ? reinterpret_cast<const double2 *>(src.K + o)[1] : make_double2(0., 0.);
+                    const int4 l4 = ok ? *reinterpret_cast<const int4 *>(src.li + o) : make_int4(-1, -1, -1, -1);
+                    acc[i][0] = k0.x; acc[i][1] = k0.y; acc[i][2] = k1.x; acc[i][3] = k1.y;
+                    li[i][0] = l4.x; li[i][1] = l4.y; li[i][2] = l4.z; li[i][3] = l4.w;
                 }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; i++)
+#pragma unroll
+                    for (int j = 0; j < TC; j++) {
+                        const int col = TC * cg + j;
+                        const bool ok = 8 * rg + i < N && col < wJ;
+                        const int64_t o = (int64_t)prow[i] * N + c0 + col;
+                        acc[i][j] = ok ? src.K[o] : 0.;
+                        li[i][j] = ok ? src.li[o] : -1;
+                    }
+            }
 #pragma unroll
             for (int i = 0; i < 8; i++)
 #pragma unroll
@@ -944,8 +964,18 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
         const int r = t / NB, c = t - r * NB;
         dv = (r < nb && c < nb) ? A[(int64_t)sm.perm[k0 + r] * N + k0 + c] : 0.;
         const double *row = A + (int64_t)sm.perm[t < k0 ? t : 0] * N + k0;
+        if ((N & 1) == 0 && nb == NB) {
+            const double2 *r2 = reinterpret_cast<const double2 *>(row);
 #pragma unroll
-        for (int m = 0; m < NB; m++) u[m] = (t < k0 && m < nb) ? row[m] : 0.;
+            for (int m = 0; m < NB / 2; m++) {
+                const double2 v = (t < k0) ? r2[m] : make_double2(0., 0.);
+                u[2 * m] = v.x;
+                u[2 * m + 1] = v.y;
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < NB; m++) u[m] = (t < k0 && m < nb) ? row[m] : 0.;
+        }
     };
     double dcur, ucur[NB], dnxt = 0., unxt[NB];
     load_blk(nblk - 1, dcur, ucur);
