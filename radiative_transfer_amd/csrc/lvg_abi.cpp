@@ -30,6 +30,8 @@ extern "C" int lvg_kernel_max_levels(void);
 extern "C" hipError_t lvg_kernel_occupancy(int *blocks_per_cu);
 extern "C" hipError_t lvg_launch_lum(const LvgDevProblem *P, const LvgLaunch *L, const LvgLumArgs *A, int grid,
                                      int nb_trans, int nb_lay, hipStream_t s);
+extern "C" hipError_t lvg_sched_order(const double *soa, int ld, int n, double *keys, double *keys_sorted, int *idx,
+                                      int *order, void *temp, size_t *temp_bytes, hipStream_t s);
 extern "C" hipError_t lvg_tr_launch(int stage, const void *args_dev, int nb_lines, int nb_lay, int nb_sel, hipStream_t s);
 
 namespace {
@@ -68,6 +70,9 @@ struct lvg_handle {
     double *d_soa = nullptr, *d_pops = nullptr;
     void *d_status = nullptr;
     size_t soa_cap = 0, pops_cap = 0, status_cap = 0;
+    // layer scheduling order (lvg_sched.hip)
+    void *d_sched = nullptr, *d_sched_tmp = nullptr;
+    size_t sched_cap = 0, sched_tmp_cap = 0;
     double last_ms = 0.;
     int last_launches = 0;
     // device-resident parameter blocks (kernels take pointers: no kernarg copies)
@@ -629,6 +634,8 @@ void lvg_destroy(lvg_handle *h) {
     if (h->d_status) (void)hipFree(h->d_status);
     if (h->d_prob) (void)hipFree(h->d_prob);
     if (h->d_launch) (void)hipFree(h->d_launch);
+    if (h->d_sched) (void)hipFree(h->d_sched);
+    if (h->d_sched_tmp) (void)hipFree(h->d_sched_tmp);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -705,6 +712,18 @@ int lvg_solve_layers_device(lvg_handle *h, int nb_lay, const double *d_soa, doub
     L.soa = d_soa;
     L.pops = d_pops;
     L.status = d_status;
+    if (nb_lay > grid && !std::getenv("LVG_INDEX_ORDER")) {
+        // longest-expected-first order of the work queue (lvg_sched.hip); results do not
+        // depend on it. Scratch: keys, sorted keys (double), indices, order (int).
+        size_t tmp = 0;
+        HIPCHECK(h, lvg_sched_order(nullptr, nb_lay, nb_lay, nullptr, nullptr, nullptr, nullptr, nullptr, &tmp, s));
+        if ((rc = grow(h, &h->d_sched, &h->sched_cap, (size_t)nb_lay * (2 * sizeof(double) + 2 * sizeof(int))))) return rc;
+        if ((rc = grow(h, &h->d_sched_tmp, &h->sched_tmp_cap, std::max<size_t>(tmp, 1)))) return rc;
+        double *keys = static_cast<double *>(h->d_sched), *keys2 = keys + nb_lay;
+        int *idx = reinterpret_cast<int *>(keys2 + nb_lay), *order = idx + nb_lay;
+        HIPCHECK(h, lvg_sched_order(d_soa, nb_lay, nb_lay, keys, keys2, idx, order, h->d_sched_tmp, &tmp, s));
+        L.order = order;
+    }
     const LvgLaunch *dL = nullptr;
     if ((rc = push_launch(h, L, 0, s, &dL))) return rc;
     HIPCHECK(h, hipMemsetAsync(h->counter, 0, sizeof(int), s));

@@ -89,6 +89,7 @@ struct LvgLaunch {
     double   *ws;                     // [nb_slots][ws_stride]
     int64_t   ws_stride;
     int      *counter;                // work queue head
+    const int *order;                 // queue position -> layer (NULL: index order)
     // debug probe outputs (lvg_debug_calc_new_pop)
     double   *dbg_matrix, *dbg_df, *dbg_pop_in;
     int       dbg_mode;               // 0 solve, 1 debug calc_new_pop, 2 boundary pops only

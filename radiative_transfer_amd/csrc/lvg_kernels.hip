@@ -102,7 +102,7 @@ struct Smem {
     int8_t tet[LVG_MAX_CLASSES], tgrp[LVG_MAX_CLASSES];
     double dust[LVG_MAX_DUST];
     double hist_acc[32];
-    int    layer;
+    int    layer, pidx;
 };
 
 // ------------------------------------------------------------------------------
@@ -1300,11 +1300,15 @@ __global__ void __launch_bounds__(BT, 2) solve_kernel(const LvgDevProblem *__res
     load_rule_table(P, sm);
     Slot S = make_slot(P, Lc, blockIdx.x);
     for (;;) {
-        if (threadIdx.x == 0) sm.layer = atomicAdd(Lc.counter, 1);
+        if (threadIdx.x == 0) {
+            const int q = atomicAdd(Lc.counter, 1);
+            sm.layer = (q < Lc.nb_lay && Lc.order) ? Lc.order[q] : q;
+            sm.pidx = q;
+        }
         __syncthreads();
-        const int l = sm.layer;
+        const int l = sm.layer, q = sm.pidx;
         __syncthreads();
-        if (l >= Lc.nb_lay) break;
+        if (q >= Lc.nb_lay) break;
         solve_layer(P, Lc, l, S, sm);
     }
 }
