@@ -32,19 +32,28 @@ namespace lvg {
 // thread 0 of every block, flushed to lvg_phase_cycles[]. Never in the product .so.
 #ifdef LVG_PHASE_TIMERS
 enum { PH_SETUP, PH_BOUNDARY, PH_LINES, PH_ASSEMBLE, PH_PANEL, PH_TRSM, PH_GEMM, PH_BACKSUB, PH_CTL,
-       PH_LSETUP, PH_PAIRS, PH_BDIAG, PH_BLOAD, PH_CLK_MEMTIME, PH_CLK_REALTIME, PH_N };
-__device__ unsigned long long lvg_phase_cycles[16];
+       PH_LSETUP, PH_PAIRS, PH_BDIAG, PH_BLOAD, PH_CLK_MEMTIME, PH_CLK_REALTIME, PH_RSV,
+       PH_T_FETCH, PH_T_SOLVE, PH_T_STAGE, PH_P_RED, PH_P_POST, PH_P_WB, PH_N };
+__device__ unsigned long long lvg_phase_cycles[32];
 #define TSTAMP(v) unsigned long long v = __builtin_amdgcn_s_memtime()
 #define RSTAMP(v) unsigned long long v = __builtin_amdgcn_s_memrealtime()
+// sums kept in LDS by thread 0 (no global atomics inside the timed code: queued
+// atomics would hold up the vmcnt waits of later loads), flushed once per block
+__shared__ unsigned long long lvg_ph_lds[32];
 #define RACC(ph, v0) do { if (threadIdx.x == 0) { unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); \
-    atomicAdd(&lvg_phase_cycles[ph], t_ - (v0)); } } while (0)
+    lvg_ph_lds[ph] += t_ - (v0); } } while (0)
 #define TACC(ph, v0) do { if (threadIdx.x == 0) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-    atomicAdd(&lvg_phase_cycles[ph], t_ - (v0)); } } while (0)
+    lvg_ph_lds[ph] += t_ - (v0); } } while (0)
+#define PH_INIT() do { if (threadIdx.x < 32) lvg_ph_lds[threadIdx.x] = 0; __syncthreads(); } while (0)
+#define PH_FLUSH() do { __syncthreads(); if (threadIdx.x < 32 && lvg_ph_lds[threadIdx.x]) \
+    atomicAdd(&lvg_phase_cycles[threadIdx.x], lvg_ph_lds[threadIdx.x]); } while (0)
 #else
 #define TSTAMP(v) do {} while (0)
 #define TACC(ph, v0) do {} while (0)
 #define RSTAMP(v) do {} while (0)
 #define RACC(ph, v0) do {} while (0)
+#define PH_INIT() do {} while (0)
+#define PH_FLUSH() do {} while (0)
 #endif
 
 constexpr int BT   = 256;   // threads per workgroup
@@ -83,8 +92,8 @@ struct Smem {
     double cand[2][NW][NB + 1]; // panel: each wave's pivot candidate row and its b, double buffered
     int    candp[2][NW];        // its physical row
     double L11[NB][NB + 1];
-    double Ub[NB][WB + 2];      // U rows of one chunk across the block column
-    union {
+    alignas(16) double Ub[NB][WB + 2];   // U rows of one chunk across the block column
+    union alignas(16) {
         double P[NMAX][NB + 1]; // panel, physical rows
         double LT[NB][NMAX];    // L of one chunk, transposed, physical rows
     } pu;
@@ -108,6 +117,20 @@ struct Smem {
 // ------------------------------------------------------------------------------
 // small helpers
 // ------------------------------------------------------------------------------
+// L2 prefetch: an ordinary dword load whose value is kept alive by an empty asm
+// use; the compiler tracks it like any load (vmcnt), so no VGPR is reused early.
+#ifndef LVG_GEMM_B128
+#define LVG_GEMM_B128 1
+#endif
+#ifndef LVG_PANEL_BALLOT
+#define LVG_PANEL_BALLOT 1
+#endif
+#ifndef LVG_L2_PREFETCH
+#define LVG_L2_PREFETCH 0
+#endif
+__device__ __forceinline__ int l2_token(const void *p) { return *reinterpret_cast<const int *>(p); }
+__device__ __forceinline__ void l2_token_use(int x) { asm volatile("" ::"v"(x)); }
+
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
@@ -630,10 +653,21 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
             const double av = fabs(rw[c]);
             const unsigned long long bits = (act && av == av) ? (unsigned long long)__double_as_longlong(av) : 0ull;
             const unsigned hi = act ? ((unsigned)(bits >> 32) | 0x80000000u) : 0u, lo = (unsigned)bits;
+            TSTAMP(tpr);
             const unsigned H = wave_max_u32(hi);
-            const unsigned Lw = wave_max_u32(hi == H ? lo : 0u);
-            const unsigned X = wave_max_u32((hi == H && lo == Lw && act) ? ~(unsigned)lp : 0u);
-            const int wmin = (int)~X;
+            unsigned Lw;
+            int wmin;
+            const unsigned long long tie = LVG_PANEL_BALLOT ? __ballot(hi == H) : 0ull;
+            if (LVG_PANEL_BALLOT && __popcll(tie) == 1) {
+                // one lane holds the wave's maximum upper word: it is the candidate
+                const int ln = __ffsll((long long)tie) - 1;
+                Lw = (unsigned)__builtin_amdgcn_readlane((int)lo, ln);
+                wmin = __builtin_amdgcn_readlane(lp, ln);
+            } else {
+                Lw = wave_max_u32(hi == H ? lo : 0u);
+                const unsigned X = wave_max_u32((hi == H && lo == Lw && act) ? ~(unsigned)lp : 0u);
+                wmin = (int)~X;
+            }
             if ((t & 63) == 0) {
                 sm.pkey[4 * buf + w] = ((unsigned long long)H << 32) | Lw;
                 sm.ired[4 * buf + w] = wmin;
@@ -644,6 +678,8 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
                 sm.cand[buf][w][NB] = rb;
             }
             __syncthreads();                       // one barrier per column
+            TACC(PH_P_RED, tpr);
+            TSTAMP(tpp);
             // the four candidates at once, winner picked without branches
             unsigned long long ok[NW];
             int oi[NW];
@@ -671,8 +707,10 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
                 for (int j = 0; j < NB; j++) if (j > c) rw[j] = fma(-l, prow[j], rw[j]);
                 rb = fma(-l, bc, rb);
             }
+            TACC(PH_P_POST, tpp);
         }
     }
+    TSTAMP(tpw);
     __syncthreads();
     if (part) {
         // rows of this chunk and below: factors back to A (physical row p)
@@ -690,6 +728,7 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
         for (int j = 0; j < NB; j++) sm.pu.P[p][j] = rw[j];
     }
     __syncthreads();
+    TACC(PH_P_WB, tpw);
 }
 
 __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Smem &sm, const LuSrc &src, const bool FUSED) {
@@ -697,6 +736,12 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
     const int rg = t >> 3, cg = t & 7;
     double s_acc = (t == 0) ? 1. : 0.;             // residual row t (FUSED)
     for (int i = t; i < N; i += BT) { sm.perm[i] = i; sm.pos[i] = i; }
+    // L2 prefetch tokens: one dword per 128-byte line of the slot's operands read
+    // next (the next block column of K/li or A, the next chunk of L), so the loads
+    // that need them later hit L2 instead of HBM. Each token is consumed (waited on)
+    // only when the next prefetch of its kind is issued, long after it has landed.
+    int pf_blk0 = 0, pf_blk1 = 0, pf_blk2 = 0, pf_l = 0;
+    const int prow_t = t < N ? t : 0;
     __syncthreads();
     for (int c0 = 0; c0 < N; c0 += WB) {
         TSTAMP(tp0);
@@ -710,6 +755,22 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
 #pragma unroll
         for (int i = 0; i < 8; i++) prow[i] = (8 * rg + i < N) ? sm.perm[8 * rg + i] : 0;
         const int trow = (t < N) ? sm.perm[t] : 0;   // physical row of tile row t (L staging)
+        if (LVG_L2_PREFETCH) {
+            l2_token_use(pf_blk0); l2_token_use(pf_blk1); l2_token_use(pf_blk2); l2_token_use(pf_l);
+            if (c0 > 0) pf_l = l2_token(A + (int64_t)trow * N);                    // L of chunk 0
+            const int cn = c0 + WB;                                                  // next block column
+            if (cn < N) {
+                const int64_t o = (int64_t)prow_t * N + cn;
+                if (FUSED) {
+                    pf_blk0 = l2_token(src.K + o);
+                    pf_blk1 = l2_token(src.K + o + 16);
+                    pf_blk2 = l2_token(src.li + o);
+                } else {
+                    pf_blk0 = l2_token(A + o);
+                    pf_blk1 = l2_token(A + o + 16);
+                }
+            }
+        }
         // ---- block column c0..c0+wJ-1 into registers (physical rows, coalesced)
         if (!FUSED) {
 #pragma unroll
@@ -841,6 +902,10 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                 } else {
                     fetch_l(kk, lrow, l11v);
                 }
+                if (LVG_L2_PREFETCH && kk + NB < c0) {
+                    l2_token_use(pf_l);
+                    pf_l = l2_token(A + (int64_t)trow * N + kk + NB);                  // L of the next chunk
+                }
             } else {
                 const bool la = t < N && sm.pos[trow] >= kk + nb;
 #pragma unroll
@@ -860,6 +925,8 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             }
             if (kk < c0 && t < NB * NB) sm.L11[t / NB][t % NB] = l11v;
             __syncthreads();
+            TACC(PH_T_FETCH, tp2);
+            TSTAMP(tp2s);
             // ---- TRSM U = L11^-1 Ub: wave w owns columns [WB/4*w, WB/4*(w+1)), lane l row
             //      l&15 of TC/2 of them; x_r takes its updates for m ascending (oracle
             //      order), x_m broadcast within the 16-lane row by DPP. U rows to A for back
@@ -897,10 +964,13 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                     }
                 }
             }
+            TACC(PH_T_SOLVE, tp2s);
+            TSTAMP(tp2t);
             // ---- staged L, transposed (thread per row: conflict-free LDS writes)
 #pragma unroll
             for (int m = 0; m < NB; m++) sm.pu.LT[m][t] = lrow[m];
             __syncthreads();
+            TACC(PH_T_STAGE, tp2t);
             have_next = LVG_PREFETCH_L && kk + NB < c0;
             if (have_next) fetch_l(kk + NB, lnext, l11next);
             TACC(PH_TRSM, tp2);
@@ -920,10 +990,20 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                 // operands of step m+1 are read from LDS while step m computes
                 double a0[8], u0[TC], a1[8], u1[TC];
                 auto ld = [&](int m, double (&a)[8], double (&u)[TC]) {
+                    if (LVG_GEMM_B128) {
+                        // 16-byte LDS reads (ds_read_b128: half the LDS cycles of ds_read2_b64)
+                        const double2 *ap = reinterpret_cast<const double2 *>(&sm.pu.LT[m][8 * rg]);
+                        const double2 *up = reinterpret_cast<const double2 *>(&sm.Ub[m][TC * cg]);
 #pragma unroll
-                    for (int i = 0; i < 8; i++) a[i] = sm.pu.LT[m][8 * rg + i];
+                        for (int i = 0; i < 4; i++) { const double2 v = ap[i]; a[2 * i] = v.x; a[2 * i + 1] = v.y; }
 #pragma unroll
-                    for (int j = 0; j < TC; j++) u[j] = sm.Ub[m][TC * cg + j];
+                        for (int j = 0; j < TC / 2; j++) { const double2 v = up[j]; u[2 * j] = v.x; u[2 * j + 1] = v.y; }
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 8; i++) a[i] = sm.pu.LT[m][8 * rg + i];
+#pragma unroll
+                        for (int j = 0; j < TC; j++) u[j] = sm.Ub[m][TC * cg + j];
+                    }
                 };
                 auto upd = [&](const double (&a)[8], const double (&u)[TC]) {
 #pragma unroll
@@ -1297,6 +1377,7 @@ __global__ void __launch_bounds__(BT, 2) solve_kernel(const LvgDevProblem *__res
     __shared__ Smem sm;
     const LvgDevProblem &P = *Pp;
     const LvgLaunch &Lc = *Lp;
+    PH_INIT();
     load_rule_table(P, sm);
     Slot S = make_slot(P, Lc, blockIdx.x);
     for (;;) {
@@ -1311,6 +1392,7 @@ __global__ void __launch_bounds__(BT, 2) solve_kernel(const LvgDevProblem *__res
         if (q >= Lc.nb_lay) break;
         solve_layer(P, Lc, l, S, sm);
     }
+    PH_FLUSH();
 }
 
 // lvg_debug_calc_new_pop: one calc_new_pop for one layer (block 0 only)
@@ -1450,9 +1532,9 @@ extern "C" hipError_t lvg_kernel_occupancy(int *blocks_per_cu) {
 
 #ifdef LVG_PHASE_TIMERS
 extern "C" int lvg_debug_phase_cycles(unsigned long long *out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lvg::lvg_phase_cycles), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lvg::lvg_phase_cycles), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[16] = {0};
+        unsigned long long z[32] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(lvg::lvg_phase_cycles), z, sizeof z) != hipSuccess) return -1;
     }
     return 0;
