@@ -44,8 +44,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
-HOST_SRC = os.path.join(PKG, "host", "lvg_host.cpp")
-HOST_HDR = os.path.join(PKG, "host", "lvg_host.hpp")
+HOST_SRCS = [os.path.join(PKG, "host", f) for f in ("lvg_host.cpp", "lvg_ingest.cpp")]
+HOST_HDRS = [os.path.join(PKG, "host", f) for f in ("lvg_host.hpp", "lvg_ingest.hpp")]
 HOST_LIB = os.path.join(LIB_DIR, "liblvg_host.so")
 CXX = os.environ.get("CXX", "g++")
 
@@ -54,10 +54,10 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
     """The C++ host surface (host/lvg_host.{hpp,cpp}) over the C ABI: liblvg_host.so,
     linked against liblvg_amd.so in the same directory (rpath $ORIGIN)."""
     lib = build(verbose=verbose)
-    deps = [HOST_SRC, HOST_HDR, os.path.join(ROOT, "include", "lvg_amd.h"), lib]
+    deps = HOST_SRCS + HOST_HDRS + [os.path.join(ROOT, "include", "lvg_amd.h"), lib]
     if not force and os.path.exists(HOST_LIB) and all(os.path.getmtime(d) <= os.path.getmtime(HOST_LIB) for d in deps):
         return HOST_LIB
-    cmd = [CXX, "-std=c++17", "-O2", "-fPIC", "-shared", "-Wall", "-o", HOST_LIB + ".tmp", HOST_SRC,
+    cmd = [CXX, "-std=c++17", "-O2", "-fPIC", "-shared", "-Wall", "-o", HOST_LIB + ".tmp"] + HOST_SRCS + [
            "-L" + LIB_DIR, "-llvg_amd", "-Wl,-rpath,$ORIGIN"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

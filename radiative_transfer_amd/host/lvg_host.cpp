@@ -26,6 +26,13 @@ void skip_lines(std::istream &in, int n) {
 }  // namespace
 
 // ---- spectroscopy ---------------------------------------------------------------
+// energy_level::operator== (spectroscopy.h:57-61); rounding() as the reference's utils.h
+bool energy_level::operator==(const energy_level &o) const {
+    auto r2 = [](double x) { return (int)std::floor(2. * x + 0.5); };
+    return v == o.v && syminv == o.syminv && r2(j) == r2(o.j) && r2(k1) == r2(o.k1) && r2(k2) == r2(o.k2) &&
+           r2(hf) == r2(o.hf) && name == o.name && g == o.g;
+}
+
 einstein_coeff::einstein_coeff(const energy_diagram *di) : nb_lev(di->nb_lev) {
     storage.assign((size_t)nb_lev * nb_lev, 0.);
     rows.resize(nb_lev);
@@ -43,6 +50,17 @@ void einstein_coeff::set_line(int u, int l, double a_ul, const energy_diagram *d
 // ---- collisions -----------------------------------------------------------------
 collision_data::collision_data(int nb, const std::vector<double> &tg)
     : imax(nb * (nb - 1) / 2), jmax((int)tg.size()), nb_lev(nb), tgrid(tg) {
+    storage.assign((size_t)imax * jmax, 0.);
+    rows.resize(imax > 0 ? imax : 1);
+    for (int i = 0; i < imax; i++) rows[i] = storage.data() + (size_t)i * jmax;
+    coeff = rows.data();
+}
+
+void collision_data::allocate(int nb, int jm) {
+    nb_lev = nb;
+    imax = nb * (nb - 1) / 2;
+    jmax = jm;
+    tgrid.assign(jmax, 0.);
     storage.assign((size_t)imax * jmax, 0.);
     rows.resize(imax > 0 ? imax : 1);
     for (int i = 0; i < imax; i++) rows[i] = storage.data() + (size_t)i * jmax;

@@ -35,9 +35,12 @@ struct lvg_error : std::runtime_error {
 
 // ---- spectroscopy (spectroscopy.h:46-87, :179-190) ------------------------------
 struct energy_level {
-    int nb = 0, g = 1, v = 0;
-    double j = 0., energy = 0.;   // energy in cm^-1
+    int nb = 0, g = 1, v = 0, syminv = 0;
+    double j = 0., k1 = 0., k2 = 0., spin = 0., hf = 0., energy = 0.;   // energy in cm^-1
     std::string name;
+    // spectroscopy.h:57-64: equal if all quantum numbers coincide; ordered by energy
+    bool operator==(const energy_level &o) const;
+    bool operator<(const energy_level &o) const { return energy < o.energy && !(*this == o); }
 };
 
 class energy_diagram {
@@ -45,9 +48,15 @@ public:
     int nb_lev = 0;
     std::string mol_name;          // molecule::name, e.g. "CH3OHa" (drives the retry rule)
     double mol_mass = 0.;          // g
+    double mol_spin = 0.;          // molecule::spin (selects the spin isomer in the file readers)
+    int isotop = 1;                // molecule::isotop
     std::vector<energy_level> lev_array;
     energy_diagram(const std::string &name, double mass) : mol_name(name), mol_mass(mass) {}
+    virtual ~energy_diagram() = default;
     void add_level(const energy_level &l) { lev_array.push_back(l); nb_lev = (int)lev_array.size(); }
+    // level lookups of the molecule subclasses (spectroscopy.h:79-83); -1: not found
+    virtual int get_nb(int /*v*/, double /*j*/, double /*k*/) const { return -1; }
+    virtual int get_nb(int /*syminv*/, int /*v*/, double /*j*/, double /*k*/, double /*hf*/) const { return -1; }
 };
 
 // arr[i][j]: rate i->j, arr[u][l] = A_ul, arr[l][u] = g_u/g_l A_ul (spectroscopy.cpp:918-921)
@@ -74,10 +83,14 @@ public:
     double **coeff = nullptr;      // coeff[i][t], i = f(f-1)/2 + s (f > s): 1->0, 2->0, 2->1, ...
     int species = LVG_SP_HE;       // concentration slot used by the generic rule
     collision_data(int nb_lev, const std::vector<double> &tgrid);
+    virtual ~collision_data() = default;
     collision_data(const collision_data &) = delete;
     collision_data &operator=(const collision_data &) = delete;
     double get_max_temp() const { return tgrid.back(); }
     const double *data() const { return storage.data(); }
+protected:
+    collision_data() = default;
+    void allocate(int nb_lev, int jmax);   // zeroed coeff[imax][jmax], tgrid[jmax]
 private:
     std::vector<double> storage;
     std::vector<double *> rows;
@@ -95,10 +108,27 @@ public:
     void add_electron(collision_data *d);
     virtual ~collisional_transitions();
 };
-struct ch3oh_collisions : collisional_transitions { int rule() const override { return LVG_COLL_CH3OH; } };
-struct h2o_collisions : collisional_transitions { int rule() const override { return LVG_COLL_H2O; } };
+// The path constructors read the reference's data files (lvg_ingest.cpp):
+// coll_rates_ch3oh.cpp:444-470, coll_rates_h2o.cpp:486-513, coll_rates_oh.cpp:350-378.
+struct ch3oh_collisions : collisional_transitions {
+    ch3oh_collisions() = default;
+    // file_levels*: levels listed in the vt files / the rovibrational He file / the oH2
+    // file (the reference's fixed 256 / 150 / 100, coll_rates_ch3oh.cpp:47, :148, :373)
+    ch3oh_collisions(const std::string &path, const energy_diagram *levels, int verbosity = 0, int file_levels = 256,
+                     int file_levels_rovibr = 150, int file_levels_oh2 = 100);
+    int rule() const override { return LVG_COLL_CH3OH; }
+};
+struct h2o_collisions : collisional_transitions {
+    h2o_collisions() = default;
+    h2o_collisions(const std::string &path, const energy_diagram *levels, bool he_is_scaled, int verbosity = 0);
+    int rule() const override { return LVG_COLL_H2O; }
+};
 struct oh_collisions : collisional_transitions { int rule() const override { return LVG_COLL_OH; } };
-struct oh_hf_collisions : collisional_transitions { int rule() const override { return LVG_COLL_OH_HF; } };
+struct oh_hf_collisions : collisional_transitions {
+    oh_hf_collisions() = default;
+    oh_hf_collisions(const std::string &path, const energy_diagram *levels, int verbosity = 0);
+    int rule() const override { return LVG_COLL_OH_HF; }
+};
 
 // ---- dust (dust_model.cpp:473-490, :834-841) ------------------------------------
 class dust_component {
@@ -141,8 +171,10 @@ public:
 // ---- cloud (cloud_data.h:23-60) ------------------------------------------------
 class cloud_layer {
 public:
-    double temp_n = 0., temp_el = 0., el_conc = 0., h_conc = 0., ph2_conc = 0., oh2_conc = 0.,
-           he_conc = 0., mol_conc = 0., vel_turb = 0., velg_n = 0.;
+    double zl = 0., zu = 0., dz = 0., zm = 0.;   // layer coordinates, cm
+    double temp_n = 0., temp_el = 0., av_temp_d = 0., vel_n = 0., tot_h_conc = 0., h2_opr = 0.,
+           el_conc = 0., h_conc = 0., ph2_conc = 0., oh2_conc = 0., he_conc = 0., mol_conc = 0.,
+           vel_turb = 0., velg_n = 0.;
     std::vector<double> dust_grain_conc, dust_grain_temp;
 };
 
@@ -151,6 +183,10 @@ public:
     int nb_lay = 0;
     std::vector<cloud_layer> lay_array;
     void add_layer(const cloud_layer &l) { lay_array.push_back(l); nb_lay = (int)lay_array.size(); }
+    void remove_layer(int i) { lay_array.erase(lay_array.begin() + i); nb_lay = (int)lay_array.size(); }
+    void delete_layers() { lay_array.clear(); nb_lay = 0; }
+    void set_vel_turb(double vt) { for (auto &l : lay_array) l.vel_turb = vt; }
+    double get_height() const { return lay_array.back().zu - lay_array.front().zl; }   // cloud_data.cpp:106
 };
 
 // Packed SoA view of a cloud (the ABI's lvg_layers); keeps its buffers alive.
