@@ -25,6 +25,10 @@
 #include "lvg_device.h"
 
 extern "C" hipError_t lvg_launch_solve(const LvgDevProblem *P, const LvgLaunch *L, int grid, hipStream_t s);
+extern "C" int lvg_wave_plan(int N, int nb_y, int grid_doubles, size_t lds_cap, int *wpb, size_t *dyn);
+extern "C" hipError_t lvg_wave_occupancy(int N, int wpb, size_t dyn, int *blocks_per_cu);
+extern "C" hipError_t lvg_launch_solve_wave(const LvgDevProblem *P, const LvgLaunch *L, int N, int grid, int wpb,
+                                            size_t dyn, hipStream_t s);
 extern "C" hipError_t lvg_launch_debug(const LvgDevProblem *P, const LvgLaunch *L, hipStream_t s);
 extern "C" int lvg_kernel_max_levels(void);
 extern "C" hipError_t lvg_kernel_occupancy(int *blocks_per_cu);
@@ -66,6 +70,8 @@ struct lvg_handle {
     size_t ws_bytes = 0;
     int64_t ws_stride = 0;
     int *counter = nullptr;
+    size_t lds_cap = 0;            // LDS bytes per workgroup (wave kernel plan)
+    int last_kernel = 0;           // 0 block kernel, 1 wave kernel (last solve)
     // scratch for host-buffer solves
     double *d_soa = nullptr, *d_pops = nullptr;
     void *d_status = nullptr;
@@ -668,6 +674,7 @@ int lvg_create(const lvg_problem *prob, int device, lvg_handle **out) {
             rc = fail(h, LVG_E_DEVICE, "device setup failed");
         else {
             h->cus = prop.multiProcessorCount;
+            h->lds_cap = prop.sharedMemPerBlock;
             if (hipMalloc(&h->d_prob, sizeof(LvgDevProblem)) != hipSuccess ||
                 hipMemcpy(h->d_prob, &h->P, sizeof(LvgDevProblem), hipMemcpyHostToDevice) != hipSuccess)
                 rc = fail(h, LVG_E_DEVICE, "problem block upload failed");
@@ -702,8 +709,27 @@ int lvg_solve_layers_device(lvg_handle *h, int nb_lay, const double *d_soa, doub
         const int v = std::atoi(e);
         if (v >= 1 && v <= h->blocks_per_cu) per_cu = v;
     }
-    const int grid = std::max(1, std::min(nb_lay, h->cus * per_cu));
-    if ((rc = ensure_workspace(h, grid))) return rc;
+    // kernel choice: one wave per layer for N <= 64 (lvg_wave.h), else one block per layer.
+    // Both give bit-identical results; LVG_BLOCK_KERNEL=1 forces the block kernel.
+    int wpb = 0, wave_bpc = 0;
+    size_t wdyn = 0;
+    {
+        const LvgModeLines &mh = o->line_overlap ? h->P.overlap : h->P.plain;
+        const int grid_dbl = h->P.esc_nd + h->P.esc_ng +
+                             (o->line_overlap ? h->P.ov_nd + h->P.ov_ndx + h->P.ov_ngr + h->P.ov_ng : 0);
+        const char *force = std::getenv("LVG_BLOCK_KERNEL");
+        if (!(force && force[0] == '1') && lvg_wave_plan(h->N, 2 * mh.nb_lines, grid_dbl, h->lds_cap, &wpb, &wdyn) &&
+            lvg_wave_occupancy(h->N, wpb, wdyn, &wave_bpc) == hipSuccess && wave_bpc >= 1) {
+        } else {
+            wpb = 0;
+        }
+    }
+    const bool wave = wpb > 0;
+    const int grid = wave ? std::max(1, std::min((nb_lay + wpb - 1) / wpb, h->cus * wave_bpc))
+                          : std::max(1, std::min(nb_lay, h->cus * per_cu));
+    const int slots = wave ? grid * wpb : grid;
+    h->last_kernel = wave ? 1 : 0;
+    if ((rc = ensure_workspace(h, slots))) return rc;
     LvgLaunch L;
     fill_launch(h, L, o);
     L.nb_lay = nb_lay;
@@ -712,7 +738,7 @@ int lvg_solve_layers_device(lvg_handle *h, int nb_lay, const double *d_soa, doub
     L.soa = d_soa;
     L.pops = d_pops;
     L.status = d_status;
-    if (nb_lay > grid && !std::getenv("LVG_INDEX_ORDER")) {
+    if (nb_lay > slots && !std::getenv("LVG_INDEX_ORDER")) {
         // longest-expected-first order of the work queue (lvg_sched.hip); results do not
         // depend on it. Scratch: keys, sorted keys (double), indices, order (int).
         size_t tmp = 0;
@@ -728,7 +754,8 @@ int lvg_solve_layers_device(lvg_handle *h, int nb_lay, const double *d_soa, doub
     if ((rc = push_launch(h, L, 0, s, &dL))) return rc;
     HIPCHECK(h, hipMemsetAsync(h->counter, 0, sizeof(int), s));
     HIPCHECK(h, hipEventRecord(h->ev0, s));
-    HIPCHECK(h, lvg_launch_solve(h->d_prob, dL, grid, s));
+    if (wave) HIPCHECK(h, lvg_launch_solve_wave(h->d_prob, dL, h->N, grid, wpb, wdyn, s));
+    else HIPCHECK(h, lvg_launch_solve(h->d_prob, dL, grid, s));
     HIPCHECK(h, hipEventRecord(h->ev1, s));
     h->last_launches = 1;
     if (!stream) {

@@ -242,17 +242,27 @@ __device__ __forceinline__ int locate_index(const double *a, int n, double x) {
 }
 
 // lvg_method_data::get_esc_func (lvg_method_functions.cpp:74-110)
-__device__ __forceinline__ double esc_func(const LvgDevProblem &P, double gamma, double delta) {
+// Grids the escape-probability lookups bisect: the problem's global copies (block
+// kernel) or LDS copies (wave kernel, lvg_wave.h); the tables stay in HBM/L2.
+struct EscGrids {
+    const double *ed, *eg;                 // esc_delta, esc_gamma
+    const double *old, *odx, *ogr, *og;    // ov_ld, ov_dx, ov_gr, ov_g
+};
+__device__ __forceinline__ EscGrids global_grids(const LvgDevProblem &P) {
+    return EscGrids{P.esc_delta, P.esc_gamma, P.ov_ld, P.ov_dx, P.ov_gr, P.ov_g};
+}
+
+__device__ __forceinline__ double esc_func(const LvgDevProblem &P, const EscGrids &G, double gamma, double delta) {
     const int nd = P.esc_nd, ng = P.esc_ng;
-    int k = locate_index(P.esc_delta, nd, delta);
-    int l = locate_index(P.esc_gamma, ng, gamma);
+    int k = locate_index(G.ed, nd, delta);
+    int l = locate_index(G.eg, ng, gamma);
     double t, u;
     if (k < 0) { t = 0.; k = 0; }
     else if (k > nd - 2) { t = 1.; k = nd - 2; }
-    else t = (delta - P.esc_delta[k]) / (P.esc_delta[k + 1] - P.esc_delta[k]);
+    else t = (delta - G.ed[k]) / (G.ed[k + 1] - G.ed[k]);
     if (l < 0) { l = 0; u = 0.; }
     else if (l > ng - 2) { l = ng - 2; u = 1.; }
-    else u = (gamma - P.esc_gamma[l]) / (P.esc_gamma[l + 1] - P.esc_gamma[l]);
+    else u = (gamma - G.eg[l]) / (G.eg[l + 1] - G.eg[l]);
     const double *p = P.esc_p;
     double e = p[k * ng + l] * (1. - t) * (1. - u) + p[(k + 1) * ng + l] * t * (1. - u)
              + p[k * ng + l + 1] * (1. - t) * u + p[(k + 1) * ng + l + 1] * u * t;
@@ -261,26 +271,26 @@ __device__ __forceinline__ double esc_func(const LvgDevProblem &P, double gamma,
 
 // lvg_line_overlap_data::get_esc_func (lvg_method_functions.cpp:324-392); the
 // 16 terms in the reference's order, each weighted (u, t, p, y) left to right
-__device__ __forceinline__ double overlap_esc_func(const LvgDevProblem &P, const double *tab, double gamma,
-                                                   double delta, double gratio, double dxv) {
+__device__ __forceinline__ double overlap_esc_func(const LvgDevProblem &P, const EscGrids &G, const double *tab,
+                                                   double gamma, double delta, double gratio, double dxv) {
     delta = lvg_log10(delta);
-    int m = locate_index(P.ov_ld, P.ov_nd, delta);
-    int l = locate_index(P.ov_g, P.ov_ng, gamma);
-    int k = locate_index(P.ov_gr, P.ov_ngr, gratio);
-    int n = locate_index(P.ov_dx, P.ov_ndx, dxv);
+    int m = locate_index(G.old, P.ov_nd, delta);
+    int l = locate_index(G.og, P.ov_ng, gamma);
+    int k = locate_index(G.ogr, P.ov_ngr, gratio);
+    int n = locate_index(G.odx, P.ov_ndx, dxv);
     double y = 0., u = 0., t = 0., p = 0.;
     if (m < 0) m = 0;
     else if (m > P.ov_nd - 2) { m = P.ov_nd - 2; y = 1.; }
-    else y = (delta - P.ov_ld[m]) / (P.ov_ld[m + 1] - P.ov_ld[m]);
+    else y = (delta - G.old[m]) / (G.old[m + 1] - G.old[m]);
     if (n < 0) n = 0;
     else if (n > P.ov_ndx - 2) { p = 1.; n = P.ov_ndx - 2; }
-    else p = (dxv - P.ov_dx[n]) / (P.ov_dx[n + 1] - P.ov_dx[n]);
+    else p = (dxv - G.odx[n]) / (G.odx[n + 1] - G.odx[n]);
     if (l < 0) l = 0;
     else if (l > P.ov_ng - 2) { l = P.ov_ng - 2; u = 1.; }
-    else u = (gamma - P.ov_g[l]) / (P.ov_g[l + 1] - P.ov_g[l]);
+    else u = (gamma - G.og[l]) / (G.og[l + 1] - G.og[l]);
     if (k < 0) k = 0;
     else if (k > P.ov_ngr - 2) { t = 1.; k = P.ov_ngr - 2; }
-    else t = (gratio - P.ov_gr[k]) / (P.ov_gr[k + 1] - P.ov_gr[k]);
+    else t = (gratio - G.ogr[k]) / (G.ogr[k + 1] - G.ogr[k]);
     const int W = P.ov_ngr * P.ov_ng, ndx = P.ov_ndx, ng = P.ov_ng;
     double e = 0.;
 #pragma unroll
@@ -299,9 +309,10 @@ __device__ __forceinline__ double overlap_esc_func(const LvgDevProblem &P, const
 // ------------------------------------------------------------------------------
 // layer setup: iteration_scheme_lvg::set_parameters / set_gas_param
 // ------------------------------------------------------------------------------
-__device__ __forceinline__ void layer_setup(const LvgDevProblem &P, const LvgLaunch &Lc, int l, Smem &sm) {
-    const int t = threadIdx.x;
-    if (t == 0) {
+// the layer's scalars into sm (one thread; SM: Smem or the wave kernel's WaveLayer)
+template <class SM>
+__device__ __forceinline__ void layer_scalars(const LvgDevProblem &P, const LvgLaunch &Lc, int l, SM &sm) {
+    {
         const int64_t ld = Lc.soa_ld;
         const double *s = Lc.soa + Lc.lay_offset + l;
         double T = s[0 * ld], Te = s[1 * ld];
@@ -346,6 +357,10 @@ __device__ __forceinline__ void layer_setup(const LvgDevProblem &P, const LvgLau
             sm.tx[tb] = sm.teff[tb] - tg[lo];
         }
     }
+}
+
+__device__ __forceinline__ void layer_setup(const LvgDevProblem &P, const LvgLaunch &Lc, int l, Smem &sm) {
+    if (threadIdx.x == 0) layer_scalars(P, Lc, l, sm);
     __syncthreads();
 }
 
@@ -479,14 +494,16 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
 // ------------------------------------------------------------------------------
 // radiative terms: intensity_calc (iteration_lvg.cpp:163-185, :428-501)
 // ------------------------------------------------------------------------------
-__device__ __forceinline__ double dust_opacity(const LvgDevProblem &P, const LvgModeLines &M, const Smem &sm, int n) {
+template <class SM>
+__device__ __forceinline__ double dust_opacity(const LvgDevProblem &P, const LvgModeLines &M, const SM &sm, int n) {
     double a = 0.;
     for (int c = 0; c < P.nb_comp; c++) a += M.line_sigma[(int64_t)c * M.nb_lines + n] * sm.dust[c];
     return a;
 }
 
-__device__ __forceinline__ double intensity_single(const LvgDevProblem &P, const LvgModeLines &M, const Smem &sm,
-                                                   int n, const double *pop) {
+template <class SM>
+__device__ __forceinline__ double intensity_single(const LvgDevProblem &P, const EscGrids &G, const LvgModeLines &M,
+                                                   const SM &sm, int n, const double *pop) {
     const int u = M.line_u[n], l = M.line_l[n];
     const double energy = M.line_e[n];
     const double c = sm.nmol / (EIGHT_PI * sm.vw * energy * energy * energy);
@@ -496,11 +513,12 @@ __device__ __forceinline__ double intensity_single(const LvgDevProblem &P, const
     const double dop = dust_opacity(P, M, sm, n);
     const double gamma = fabs(sm.vgrad) / (sm.vw * opac);
     const double delta = fabs(sm.vgrad) / (sm.vw * dop);
-    return emiss / opac * esc_func(P, gamma, delta);
+    return emiss / opac * esc_func(P, G, gamma, delta);
 }
 
-__device__ __forceinline__ void intensity_pair(const LvgDevProblem &P, const LvgModeLines &M, const Smem &sm,
-                                               int n1, int n2, const double *pop, double &i1, double &i2) {
+template <class SM>
+__device__ __forceinline__ void intensity_pair(const LvgDevProblem &P, const EscGrids &G, const LvgModeLines &M,
+                                               const SM &sm, int n1, int n2, const double *pop, double &i1, double &i2) {
     const double max_dx = 4.;
     const int u1 = M.line_u[n1], l1 = M.line_l[n1], u2 = M.line_u[n2], l2 = M.line_l[n2];
     const double energy = M.line_e[n1];
@@ -517,12 +535,12 @@ __device__ __forceinline__ void intensity_pair(const LvgDevProblem &P, const Lvg
     if (sm.vgrad < 0.) dx *= -1.;
     double ep1 = 0., ep2 = 0., ep01 = 0., ep02 = 0.;
     if (fabs(dx) < max_dx) {
-        ep1 = overlap_esc_func(P, P.ov_p1, g1, delta, g2 / g1, dx);
-        ep2 = overlap_esc_func(P, P.ov_p1, g2, delta, g1 / g2, -dx);
+        ep1 = overlap_esc_func(P, G, P.ov_p1, g1, delta, g2 / g1, dx);
+        ep2 = overlap_esc_func(P, G, P.ov_p1, g2, delta, g1 / g2, -dx);
     }
     if (fabs(dx) > max_dx - 0.5) {
-        ep01 = esc_func(P, g1, delta);
-        ep02 = esc_func(P, g2, delta);
+        ep01 = esc_func(P, G, g1, delta);
+        ep02 = esc_func(P, G, g2, delta);
     }
     if (fabs(dx) > max_dx) { ep1 = ep01; ep2 = ep02; }
     else if (fabs(dx) > max_dx - 0.5) {
@@ -533,8 +551,8 @@ __device__ __forceinline__ void intensity_pair(const LvgDevProblem &P, const Lvg
     i1 = em1 / op1 * ep1;
     i2 = em2 / op2 * ep2;
     if (fabs(dx) < max_dx) {
-        ep1 = overlap_esc_func(P, P.ov_p2, g1, delta, g2 / g1, dx);
-        ep2 = overlap_esc_func(P, P.ov_p2, g2, delta, g1 / g2, -dx);
+        ep1 = overlap_esc_func(P, G, P.ov_p2, g1, delta, g2 / g1, dx);
+        ep2 = overlap_esc_func(P, G, P.ov_p2, g2, delta, g1 / g2, -dx);
         if (fabs(dx) > max_dx - 0.5) {
             c = 2. * (max_dx - fabs(dx));
             ep1 *= c; ep2 *= c;
@@ -547,15 +565,16 @@ __device__ __forceinline__ void intensity_pair(const LvgDevProblem &P, const Lvg
 // y[2n] = A_ul(1+I), y[2n+1] = A_lu*I for every line of the scheme
 __device__ __forceinline__ void compute_line_terms(const LvgDevProblem &P, const LvgModeLines &M, const Smem &sm,
                                                    const double *pop, double *y) {
+    const EscGrids G = global_grids(P);
     for (int q = threadIdx.x; q < M.nb_units; q += BT) {
         int n1 = M.unit_l0[q], n2 = M.unit_l1[q];
         if (n2 < 0) {
-            double I = intensity_single(P, M, sm, n1, pop);
+            double I = intensity_single(P, G, M, sm, n1, pop);
             y[2 * n1] = M.line_aul[n1] * (1. + I);
             y[2 * n1 + 1] = M.line_alu[n1] * I;
         } else {
             double i1, i2;
-            intensity_pair(P, M, sm, n1, n2, pop, i1, i2);
+            intensity_pair(P, G, M, sm, n1, n2, pop, i1, i2);
             y[2 * n1] = M.line_aul[n1] * (1. + i1);
             y[2 * n1 + 1] = M.line_alu[n1] * i1;
             y[2 * n2] = M.line_aul[n2] * (1. + i2);
@@ -1458,10 +1477,10 @@ __global__ void __launch_bounds__(BT, 2) lum_kernel(const LvgDevProblem *__restr
                 if (aij != 0. && i != lo && i != hi) {
                     const double aji = P.einst[j * N + i];
                     if (i < j && pl[i] * aij > pl[j] * aji) {
-                        const double I = intensity_single(P, M, sm, M.line_idx[i * N + j] >> 1, ip);
+                        const double I = intensity_single(P, global_grids(P), M, sm, M.line_idx[i * N + j] >> 1, ip);
                         loss += aji * (1. + I);
                     } else if (i > j && pl[i] * aij < pl[j] * aji) {
-                        const double I = intensity_single(P, M, sm, M.line_idx[j * N + i] >> 1, ip);
+                        const double I = intensity_single(P, global_grids(P), M, sm, M.line_idx[j * N + i] >> 1, ip);
                         loss += aji * I;
                     }
                 }
@@ -1503,6 +1522,8 @@ __global__ void __launch_bounds__(64) lum_reduce_kernel(const LvgLumArgs *__rest
     A.lum[tr] = s / A.height;
 }
 
+#include "lvg_wave.h"
+
 }  // namespace lvg
 
 extern "C" hipError_t lvg_launch_lum(const LvgDevProblem *P, const LvgLaunch *L, const LvgLumArgs *A, int grid,
@@ -1523,6 +1544,43 @@ extern "C" hipError_t lvg_launch_debug(const LvgDevProblem *P, const LvgLaunch *
     hipLaunchKernelGGL(lvg::debug_kernel, dim3(1), dim3(lvg::BT), 0, s, P, L);
     return hipGetLastError();
 }
+
+// ---- wave-per-layer kernel (lvg_wave.h) for N <= 64 ----------------------------------
+// 1 and the waves per block / dynamic LDS bytes if it applies to N levels with
+// nb_y line terms and grid_doubles escape-grid points; 0 if not.
+extern "C" int lvg_wave_plan(int N, int nb_y, int grid_doubles, size_t lds_cap, int *wpb, size_t *dyn) {
+    if (N < 2 || N > lvg::WNMAX || nb_y > lvg::WYCAP || grid_doubles > lvg::WGRID_CAP) return 0;
+    for (int w = 4; w >= 1; w >>= 1) {
+        const size_t d = lvg::wave_dyn_bytes(N, w);
+        if (sizeof(lvg::WaveShared) + d <= lds_cap) { *wpb = w; *dyn = d; return 1; }
+    }
+    return 0;
+}
+
+static const void *wave_kernel(int N) {
+    if (N <= 16) return reinterpret_cast<const void *>(&lvg::solve_wave_kernel<16>);
+    if (N <= 32) return reinterpret_cast<const void *>(&lvg::solve_wave_kernel<32>);
+    if (N <= 48) return reinterpret_cast<const void *>(&lvg::solve_wave_kernel<48>);
+    return reinterpret_cast<const void *>(&lvg::solve_wave_kernel<64>);
+}
+
+extern "C" hipError_t lvg_wave_occupancy(int N, int wpb, size_t dyn, int *blocks_per_cu) {
+    const void *k = wave_kernel(N);
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+    if (e != hipSuccess) return e;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 64 * wpb, dyn);
+}
+
+extern "C" hipError_t lvg_launch_solve_wave(const LvgDevProblem *P, const LvgLaunch *L, int N, int grid, int wpb,
+                                            size_t dyn, hipStream_t s) {
+    const dim3 g(grid), b(64 * wpb);
+    if (N <= 16) hipLaunchKernelGGL(lvg::solve_wave_kernel<16>, g, b, dyn, s, P, L);
+    else if (N <= 32) hipLaunchKernelGGL(lvg::solve_wave_kernel<32>, g, b, dyn, s, P, L);
+    else if (N <= 48) hipLaunchKernelGGL(lvg::solve_wave_kernel<48>, g, b, dyn, s, P, L);
+    else hipLaunchKernelGGL(lvg::solve_wave_kernel<64>, g, b, dyn, s, P, L);
+    return hipGetLastError();
+}
+extern "C" size_t lvg_wave_static_lds(void) { return sizeof(lvg::WaveShared); }
 
 extern "C" int lvg_kernel_max_levels(void) { return lvg::NMAX; }
 extern "C" int lvg_kernel_block_threads(void) { return lvg::BT; }

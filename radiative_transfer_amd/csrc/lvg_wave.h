@@ -1,0 +1,695 @@
+// lvg_wave.h — wave-per-layer solver for small molecules (N <= 64), included by
+// lvg_kernels.hip inside namespace lvg (it reuses the block kernel's layer scalars,
+// line-term and iteration-control helpers).
+//
+// Why a second kernel: for N <= 64 the 256-thread block of solve_kernel keeps at most
+// N threads busy and pays a workgroup barrier per LU column (ph2o45: ≈2 K cycles a
+// column, 95 K per LU in the panel alone). Here ONE wavefront owns a layer:
+//  * lane i holds row i of the N x N rate matrix in registers (double a[NM]), so the
+//    LU needs no barrier and no LDS round trip: the pivot is a DPP u32 max (+ ballot),
+//    the pivot row is broadcast with v_readlane into SGPRs, every lane updates its own
+//    row with fma(-l, u_kj, a_ij) for k ascending (the oracle's order, bit for bit);
+//  * the collision operator K of the layer lives in LDS (row stride N|1, conflict-light),
+//    with the line-index map shared by the block's waves and the escape-table grids
+//    copied to LDS, so the per-iteration assembly, diagonal fold, residual and the
+//    escape-probability bisections never touch HBM;
+//  * four waves per block (fewer if K does not fit) work independent layers from the
+//    same atomic queue as solve_kernel.
+// The arithmetic of every step is the block kernel's (and the oracle's), in the same
+// order; results are bit-identical, which tests/test_gpu_parity.py checks.
+#pragma once
+
+constexpr int WYCAP = 512;        // line terms y per wave kept in LDS (host checks 2*nb_lines <= WYCAP)
+constexpr int WGRID_CAP = 1024;   // escape + overlap grid doubles copied to LDS (host checks)
+constexpr int WNMAX = 64;
+
+struct WaveLayer {                // per-wave LDS
+    double pold[WNMAX], pnew[WNMAX], diag[WNMAX];
+    double y[WYCAP];
+    double hist_acc[32];
+    double T, Te, vw, vgrad, nmol, ne;
+    double cc[LVG_MAX_COMBOS];
+    double teff[LVG_MAX_TABLES];
+    int    lo[LVG_MAX_TABLES];
+    const double *tcol[LVG_MAX_TABLES];
+    const double *tder[LVG_MAX_TABLES];
+    int64_t timax[LVG_MAX_TABLES];
+    double tdt[LVG_MAX_TABLES];
+    double tx[LVG_MAX_TABLES];
+    double dust[LVG_MAX_DUST];
+};
+
+struct WaveShared {               // per-block LDS (static part)
+    int8_t ttab[LVG_MAX_CLASSES][LVG_MAX_TERMS], tcombo[LVG_MAX_CLASSES][LVG_MAX_TERMS];
+    int8_t tet[LVG_MAX_CLASSES], tgrp[LVG_MAX_CLASSES];
+    double grids[WGRID_CAP];
+    WaveLayer w[4];
+};
+
+// dynamic LDS: line index map [N][N|1] (int), then K [wpb][N][N|1] (double)
+extern __shared__ double lvg_wave_dyn[];
+
+// LDS and global stores of one lane become visible to the other lanes of its wave
+// (s_waitcnt 0: the wave's own stores have completed before any lane reads them back)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// Collision operator of the layer (build_collision_operators, one pair per lane):
+// K[s][f] = down + electrons, K[f][s] = up + electrons (LDS, stride ldk); the
+// boundary matrix B (neutrals + A/2, global, stride N) when B != nullptr.
+__device__ __forceinline__ void wave_collisions(const LvgDevProblem &P, const WaveShared &sh, const WaveLayer &sm,
+                                                double *K, int ldk, double *B) {
+    const int N = P.N, M2 = N * (N - 1) / 2;
+    const double T = sm.T, Te = sm.Te;
+    for (int p = lane_id(); p < M2; p += 64) {
+        int f = (int)((1. + sqrt(1. + 8. * (double)p)) * 0.5);
+        while (f * (f - 1) / 2 > p) f--;
+        while (f * (f + 1) / 2 <= p) f++;
+        const int s = p - f * (f - 1) / 2;
+        const int cl = P.pair_class[p];
+        const int grp = sh.tgrp[cl];
+        double dn = 0., gsum = 0.;
+        int ng = 0;
+#pragma unroll
+        for (int k = 0; k < LVG_MAX_TERMS; k++) {
+            const int tb = sh.ttab[cl][k];
+            if (tb < 0) break;
+            const double r = (sm.tcol[tb][p] + sm.tder[tb][p] * sm.tx[tb]) * sm.cc[sh.tcombo[cl][k]];   // get_rate
+            if (k < grp) dn = (k == 0) ? r : dn + r;
+            else { gsum = (ng == 0) ? r : gsum + r; ng++; }
+        }
+        if (ng) dn = dn + gsum;
+        const double ef = P.energy[f], es = P.energy[s], gf = P.g[f], gs = P.g[s];
+        const double de = es - ef;
+        double un = 0.;
+        if (dn > MIN_COLLISION_RATE) un = dn * lvg_exp(de * CM_INVERSE_TO_KELVINS / T) * gf / gs;
+        else dn = 0.;
+        double dE = 0., uE = 0.;
+        const int et = sh.tet[cl];
+        if (et >= 0) {
+            dE = (sm.tcol[et][p] + sm.tder[et][p] * sm.tx[et]) * sm.ne;
+            if (dE > MIN_COLLISION_RATE) uE = dE * lvg_exp(de * CM_INVERSE_TO_KELVINS / Te) * gf / gs;
+            else dE = 0.;
+        }
+        K[s * ldk + f] = dn + dE;
+        K[f * ldk + s] = un + uE;
+        if (B) {
+            B[s * N + f] = 0.5 * P.einst[f * N + s] + dn;
+            B[f * N + s] = un;
+        }
+    }
+}
+
+// ---- line terms with the table lookups batched -------------------------------------
+// Same arithmetic as esc_func / overlap_esc_func / intensity_single / intensity_pair
+// (lvg_kernels.hip), reorganised so that a lane's independent table reads are issued
+// together: the bisections run in LDS first, then every table value the lane needs
+// is loaded in one round trip. Overlap: the p1 and p2 tables share the interpolation
+// indices (same gamma, delta, gratio, dx), so each direction is located once.
+struct OvIdx {
+    int m, n, k, l;
+    double y, p, u, t;
+};
+__device__ __forceinline__ OvIdx ov_index(const LvgDevProblem &P, const EscGrids &G, double gamma, double ldelta,
+                                          double gratio, double dxv) {
+    OvIdx o;
+    o.m = locate_index(G.old, P.ov_nd, ldelta);
+    o.l = locate_index(G.og, P.ov_ng, gamma);
+    o.k = locate_index(G.ogr, P.ov_ngr, gratio);
+    o.n = locate_index(G.odx, P.ov_ndx, dxv);
+    o.y = 0.; o.u = 0.; o.t = 0.; o.p = 0.;
+    if (o.m < 0) o.m = 0;
+    else if (o.m > P.ov_nd - 2) { o.m = P.ov_nd - 2; o.y = 1.; }
+    else o.y = (ldelta - G.old[o.m]) / (G.old[o.m + 1] - G.old[o.m]);
+    if (o.n < 0) o.n = 0;
+    else if (o.n > P.ov_ndx - 2) { o.p = 1.; o.n = P.ov_ndx - 2; }
+    else o.p = (dxv - G.odx[o.n]) / (G.odx[o.n + 1] - G.odx[o.n]);
+    if (o.l < 0) o.l = 0;
+    else if (o.l > P.ov_ng - 2) { o.l = P.ov_ng - 2; o.u = 1.; }
+    else o.u = (gamma - G.og[o.l]) / (G.og[o.l + 1] - G.og[o.l]);
+    if (o.k < 0) o.k = 0;
+    else if (o.k > P.ov_ngr - 2) { o.t = 1.; o.k = P.ov_ngr - 2; }
+    else o.t = (gratio - G.ogr[o.k]) / (G.ogr[o.k + 1] - G.ogr[o.k]);
+    return o;
+}
+__device__ __forceinline__ void ov_load(const LvgDevProblem &P, const double *tab, const OvIdx &o, double (&v)[16]) {
+    const int W = P.ov_ngr * P.ov_ng, ndx = P.ov_ndx, ng = P.ov_ng;
+#pragma unroll
+    for (int dm = 0; dm < 2; dm++)
+#pragma unroll
+        for (int dn = 0; dn < 2; dn++)
+#pragma unroll
+            for (int dk = 0; dk < 2; dk++)
+#pragma unroll
+                for (int dl = 0; dl < 2; dl++)
+                    v[8 * dm + 4 * dn + 2 * dk + dl] =
+                        tab[(int64_t)((o.m + dm) * ndx + o.n + dn) * W + (o.k + dk) * ng + o.l + dl];
+}
+__device__ __forceinline__ double ov_sum(const OvIdx &o, const double (&v)[16]) {
+    double e = 0.;
+#pragma unroll
+    for (int dm = 0; dm < 2; dm++)
+#pragma unroll
+        for (int dn = 0; dn < 2; dn++)
+#pragma unroll
+            for (int dk = 0; dk < 2; dk++)
+#pragma unroll
+                for (int dl = 0; dl < 2; dl++)
+                    e += v[8 * dm + 4 * dn + 2 * dk + dl] * (dl ? o.u : 1. - o.u) * (dk ? o.t : 1. - o.t) *
+                         (dn ? o.p : 1. - o.p) * (dm ? o.y : 1. - o.y);
+    return e > 1. ? 1. : (e < 0. ? 0. : e);
+}
+
+struct EscIdx {
+    int k, l;
+    double t, u;
+};
+__device__ __forceinline__ EscIdx esc_index(const LvgDevProblem &P, const EscGrids &G, double gamma, double delta) {
+    const int nd = P.esc_nd, ng = P.esc_ng;
+    EscIdx o;
+    o.k = locate_index(G.ed, nd, delta);
+    o.l = locate_index(G.eg, ng, gamma);
+    if (o.k < 0) { o.t = 0.; o.k = 0; }
+    else if (o.k > nd - 2) { o.t = 1.; o.k = nd - 2; }
+    else o.t = (delta - G.ed[o.k]) / (G.ed[o.k + 1] - G.ed[o.k]);
+    if (o.l < 0) { o.l = 0; o.u = 0.; }
+    else if (o.l > ng - 2) { o.l = ng - 2; o.u = 1.; }
+    else o.u = (gamma - G.eg[o.l]) / (G.eg[o.l + 1] - G.eg[o.l]);
+    return o;
+}
+__device__ __forceinline__ void esc_load(const LvgDevProblem &P, const EscIdx &o, double (&v)[4]) {
+    const int ng = P.esc_ng;
+    const double *p = P.esc_p;
+    v[0] = p[o.k * ng + o.l]; v[1] = p[(o.k + 1) * ng + o.l]; v[2] = p[o.k * ng + o.l + 1];
+    v[3] = p[(o.k + 1) * ng + o.l + 1];
+}
+__device__ __forceinline__ double esc_sum(const EscIdx &o, const double (&v)[4]) {
+    const double t = o.t, u = o.u;
+    double e = v[0] * (1. - t) * (1. - u) + v[1] * t * (1. - u) + v[2] * (1. - t) * u + v[3] * u * t;
+    return e > 1. ? 1. : (e < 0. ? 0. : e);
+}
+
+// plain scheme: WUB single-line units per lane per pass (intensity_single), stores last
+constexpr int WUB = 4;
+__device__ __forceinline__ void wave_line_terms_plain(const LvgDevProblem &P, const EscGrids &G, const LvgModeLines &M,
+                                                      WaveLayer &sm) {
+    const int t = lane_id();
+    for (int q0 = t; q0 < M.nb_units; q0 += 64 * WUB) {
+        int n[WUB];
+        double I[WUB], aul[WUB], alu[WUB];
+        EscIdx ix[WUB];
+        double em[WUB], op[WUB], tv[WUB][4];
+#pragma unroll
+        for (int b = 0; b < WUB; b++) {
+            const int q = q0 + 64 * b;
+            n[b] = (q < M.nb_units) ? M.unit_l0[q] : M.unit_l0[t];
+        }
+#pragma unroll
+        for (int b = 0; b < WUB; b++) {
+            const int nn = n[b];
+            const int u = M.line_u[nn], l = M.line_l[nn];
+            const double energy = M.line_e[nn];
+            aul[b] = M.line_aul[nn];
+            alu[b] = M.line_alu[nn];
+            const double c = sm.nmol / (EIGHT_PI * sm.vw * energy * energy * energy);
+            em[b] = c * aul[b] * sm.pold[u];
+            op[b] = c * alu[b] * sm.pold[l] - em[b] + MIN_LINE_OPACITY;
+            if (op[b] < 0.) op[b] *= INV_TRANS_FACTOR;
+            const double dop = dust_opacity(P, M, sm, nn);
+            const double gamma = fabs(sm.vgrad) / (sm.vw * op[b]);
+            const double delta = fabs(sm.vgrad) / (sm.vw * dop);
+            ix[b] = esc_index(P, G, gamma, delta);
+        }
+#pragma unroll
+        for (int b = 0; b < WUB; b++) esc_load(P, ix[b], tv[b]);
+#pragma unroll
+        for (int b = 0; b < WUB; b++) I[b] = em[b] / op[b] * esc_sum(ix[b], tv[b]);
+#pragma unroll
+        for (int b = 0; b < WUB; b++) {
+            if (q0 + 64 * b < M.nb_units) {
+                sm.y[2 * n[b]] = aul[b] * (1. + I[b]);
+                sm.y[2 * n[b] + 1] = alu[b] * I[b];
+            }
+        }
+    }
+}
+
+// overlap scheme: one unit per lane per pass; pairs through intensity_pair's sequence
+__device__ __forceinline__ void wave_line_terms_overlap(const LvgDevProblem &P, const EscGrids &G,
+                                                        const LvgModeLines &M, WaveLayer &sm) {
+    const double max_dx = 4.;
+    for (int q = lane_id(); q < M.nb_units; q += 64) {
+        const int n1 = M.unit_l0[q], n2 = M.unit_l1[q];
+        if (n2 < 0) {
+            const double I = intensity_single(P, G, M, sm, n1, sm.pold);
+            sm.y[2 * n1] = M.line_aul[n1] * (1. + I);
+            sm.y[2 * n1 + 1] = M.line_alu[n1] * I;
+            continue;
+        }
+        const double *pop = sm.pold;
+        const int u1 = M.line_u[n1], l1 = M.line_l[n1], u2 = M.line_u[n2], l2 = M.line_l[n2];
+        const double energy = M.line_e[n1];
+        double c = sm.nmol / (EIGHT_PI * sm.vw * energy * energy * energy);
+        const double a1 = M.line_aul[n1], b1 = M.line_alu[n1], a2 = M.line_aul[n2], b2 = M.line_alu[n2];
+        const double em1 = c * a1 * pop[u1];
+        double op1 = c * (b1 * pop[l1] - a1 * pop[u1]) + MIN_LINE_OPACITY;
+        const double em2 = c * a2 * pop[u2];
+        double op2 = c * (b2 * pop[l2] - a2 * pop[u2]) + MIN_LINE_OPACITY;
+        if (op1 < 0.) op1 *= INV_TRANS_FACTOR;
+        if (op2 < 0.) op2 *= INV_TRANS_FACTOR;
+        const double g1 = fabs(sm.vgrad) / (sm.vw * op1), g2 = fabs(sm.vgrad) / (sm.vw * op2);
+        const double delta = fabs(sm.vgrad) / (sm.vw * dust_opacity(P, M, sm, n1));
+        double dx = (P.energy[u1] - P.energy[l1] - P.energy[u2] + P.energy[l2]) * SPEED_OF_LIGHT / (energy * sm.vw);
+        if (sm.vgrad < 0.) dx *= -1.;
+        const bool near = fabs(dx) < max_dx, far = fabs(dx) > max_dx - 0.5;
+        double ep1 = 0., ep2 = 0., ep01 = 0., ep02 = 0., q1 = 0., q2 = 0.;
+        if (near) {
+            const double ld = lvg_log10(delta);
+            const OvIdx A = ov_index(P, G, g1, ld, g2 / g1, dx), B = ov_index(P, G, g2, ld, g1 / g2, -dx);
+            double v1[16], v2[16], w1[16], w2[16];
+            ov_load(P, P.ov_p1, A, v1);
+            ov_load(P, P.ov_p1, B, v2);
+            ov_load(P, P.ov_p2, A, w1);
+            ov_load(P, P.ov_p2, B, w2);
+            ep1 = ov_sum(A, v1);
+            ep2 = ov_sum(B, v2);
+            q1 = ov_sum(A, w1);
+            q2 = ov_sum(B, w2);
+        }
+        if (far) {
+            const EscIdx A = esc_index(P, G, g1, delta), B = esc_index(P, G, g2, delta);
+            double v1[4], v2[4];
+            esc_load(P, A, v1);
+            esc_load(P, B, v2);
+            ep01 = esc_sum(A, v1);
+            ep02 = esc_sum(B, v2);
+        }
+        if (fabs(dx) > max_dx) { ep1 = ep01; ep2 = ep02; }
+        else if (far) {
+            c = 2. * (max_dx - fabs(dx));
+            ep1 = ep01 * (1. - c) + ep1 * c;
+            ep2 = ep02 * (1. - c) + ep2 * c;
+        }
+        double i1 = em1 / op1 * ep1;
+        double i2 = em2 / op2 * ep2;
+        if (near) {
+            ep1 = q1;
+            ep2 = q2;
+            if (far) {
+                c = 2. * (max_dx - fabs(dx));
+                ep1 *= c; ep2 *= c;
+            }
+            i1 += em2 / op2 * ep1;
+            i2 += em1 / op1 * ep2;
+        }
+        sm.y[2 * n1] = a1 * (1. + i1);
+        sm.y[2 * n1 + 1] = b1 * i1;
+        sm.y[2 * n2] = a2 * (1. + i2);
+        sm.y[2 * n2 + 1] = b2 * i2;
+    }
+}
+
+// LU with partial pivoting of the register rows a (lane = physical row) and the
+// right-hand side rb, then back substitution; x[k] (LDS) receives solution k.
+// Same operation sequence as oracle_lu_solve: pivot = first maximum |a_ik| in the
+// oracle's (physically swapped) row order, tracked here as each row's logical
+// position lp; every a_ij receives fma(-l_ik, u_kj, a_ij) for k ascending; x_k =
+// b_k / u_kk and b_i = fma(-u_ik, x_k, b_i) for k descending.
+template <int NM>
+__device__ __forceinline__ void wave_lu_solve(double (&a)[NM], double rb, int N, double *x) {
+    const int ln = lane_id();
+    TSTAMP(tf0);
+    bool act = ln < N;
+    int lp = ln;
+#pragma unroll
+    for (int c = 0; c < NM; c++) {
+        if (c < N) {
+            const double av = fabs(a[c]);
+            const unsigned long long bits = (act && av == av) ? (unsigned long long)__double_as_longlong(av) : 0ull;
+            const unsigned hi = act ? ((unsigned)(bits >> 32) | 0x80000000u) : 0u, lo = (unsigned)bits;
+            const unsigned H = wave_max_u32(hi);
+            const unsigned long long tie = __ballot(hi == H);
+            int pl;
+            if (__popcll(tie) == 1) {
+                pl = __ffsll((long long)tie) - 1;
+            } else {
+                const unsigned Lw = wave_max_u32(hi == H ? lo : 0u);
+                const unsigned X = wave_max_u32((hi == H && lo == Lw && act) ? ~(unsigned)lp : 0u);
+                const int wmin = (int)~X;
+                pl = __ffsll((long long)__ballot(act && hi == H && lo == Lw && lp == wmin)) - 1;
+            }
+            pl = __builtin_amdgcn_readfirstlane(pl);
+            const int plp = __builtin_amdgcn_readlane(lp, pl);
+            const double piv = readlane_d(a[c], pl);
+            const double bc = readlane_d(rb, pl);
+            if (ln == pl) { act = false; lp = c; }
+            else if (lp == c) lp = plp;
+            const double l = a[c] / piv;
+#pragma unroll
+            for (int j = c + 1; j < NM; j++) {
+                const double u = readlane_d(a[j], pl);
+                if (act) a[j] = fma(-l, u, a[j]);
+            }
+            if (act) { a[c] = l; rb = fma(-l, bc, rb); }
+        }
+    }
+    TACC(PH_PANEL, tf0);
+    TSTAMP(tb0);
+#pragma unroll
+    for (int k = NM - 1; k >= 0; k--) {
+        if (k < N) {
+            const int ow = __builtin_amdgcn_readfirstlane(__ffsll((long long)__ballot(ln < N && lp == k)) - 1);
+            const double xk = readlane_d(rb / a[k], ow);
+            if (ln == ow) rb = xk;
+            else if (lp < k) rb = fma(-a[k], xk, rb);
+        }
+    }
+    if (ln < N) x[lp] = rb;
+    TACC(PH_BACKSUB, tb0);
+}
+
+// Rows of the boundary-layer matrix B (iteration_control.cpp:52-91) into registers:
+// diagonal = minus the ascending column sum, row 0 <- 1.
+template <int NM>
+__device__ __forceinline__ void wave_boundary_rows(const double *B, int N, double (&a)[NM]) {
+    const int ln = lane_id(), i = ln < N ? ln : 0;
+    double d = 0.;
+    for (int r = 0; r < N; r++)
+        if (r != i) d = d - B[r * N + i];
+#pragma unroll
+    for (int j = 0; j < NM; j++) {
+        double v = (j < N) ? B[i * N + j] : 0.;
+        if (j == i) v = d;
+        if (i == 0) v = 1.;
+        a[j] = v;
+    }
+}
+
+// iteration_control (iteration_control.h:84-242) per wave: as the block versions in
+// lvg_kernels.hip, with lanes for threads and wave_sync for barriers.
+__device__ __forceinline__ void wave_accel_step(Ctl &C, Slot &S, int N, WaveLayer &sm) {
+    const int t = lane_id();
+    const int np = C.nb_prev - 1;
+    const double *r0 = ring(S.res, C.hr, 0, N);
+    const double *p0 = ring(S.prev, C.hp, 0, N);
+    const int nsum = np * np + np;
+    if (t < nsum) {
+        int i, j;
+        if (t < np * np) { i = t / np; j = t - i * np; } else { i = t - np * np; j = -1; }
+        const double *ri = ring(S.res, C.hr, i + 1, N);
+        const double *rj = (j >= 0) ? ring(S.res, C.hr, j + 1, N) : nullptr;
+        double a = 0.;
+        for (int k = 0; k < N; k++) {
+            double w = p0[k] + 1.e-99;
+            double num = (j >= 0) ? (r0[k] - ri[k]) * (r0[k] - rj[k]) : (r0[k] - ri[k]) * r0[k];
+            a = a + num / (w * w);
+        }
+        sm.hist_acc[t] = a;
+    }
+    wave_sync();
+    if (t == 0) {
+        double Am[4][4], bv[4];
+        for (int i = 0; i < np; i++) {
+            for (int j = 0; j < np; j++) Am[i][j] = sm.hist_acc[i * np + j];
+            bv[i] = sm.hist_acc[np * np + i];
+        }
+        for (int k = 0; k < np; k++) {
+            int p = k;
+            double amax = fabs(Am[k][k]);
+            for (int i = k + 1; i < np; i++) if (fabs(Am[i][k]) > amax) { amax = fabs(Am[i][k]); p = i; }
+            if (p != k) {
+                for (int j = 0; j < np; j++) { double x = Am[k][j]; Am[k][j] = Am[p][j]; Am[p][j] = x; }
+                double x = bv[k]; bv[k] = bv[p]; bv[p] = x;
+            }
+            double piv = Am[k][k];
+            for (int i = k + 1; i < np; i++) {
+                double l = Am[i][k] / piv;
+                Am[i][k] = l;
+                for (int j = k + 1; j < np; j++) Am[i][j] = fma(-l, Am[k][j], Am[i][j]);
+                bv[i] = fma(-l, bv[k], bv[i]);
+            }
+        }
+        for (int k = np - 1; k >= 0; k--) {
+            bv[k] /= Am[k][k];
+            double x = bv[k];
+            for (int i = 0; i < k; i++) bv[i] = fma(-Am[i][k], x, bv[i]);
+        }
+        double sum = 0.;
+        for (int i = 0; i < np; i++) { sum = sum + bv[i]; sm.hist_acc[16 + i] = bv[i]; }
+        sm.hist_acc[31] = sum;
+    }
+    wave_sync();
+    const double sum = sm.hist_acc[31];
+    for (int k = t; k < N; k += 64) {
+        double a = (1. - sum) * p0[k];
+        for (int i = 0; i < np; i++) a = a + sm.hist_acc[16 + i] * ring(S.prev, C.hp, i + 1, N)[k];
+        sm.pold[k] = a;
+    }
+    wave_sync();
+}
+
+__device__ __forceinline__ void wave_start_pass(Ctl &C, Slot &S, const LvgLaunch &Lc, int N, int max_nb, int accel) {
+    C.acceleration = accel;
+    C.accel_start = Lc.accel_start;
+    C.accel_period = Lc.accel_period;
+    C.nb_prev = Lc.accel_nb;
+    C.max_iter = max_nb;
+    C.iter_nb = C.nb_after_accel = 0;
+    C.best_eq = 1.;
+    C.eq_error = C.pop_error = C.rel_error = 0.;
+    C.hp = C.hr = 0;
+    C.np = C.nr = 0;
+    if (lane_id() < N) S.opt[lane_id()] = 0.;
+    wave_sync();
+}
+
+__device__ __forceinline__ void wave_next_step_pre(Ctl &C, Slot &S, int N, WaveLayer &sm) {
+    const int t = lane_id();
+    C.hp = (C.hp + NHIST - 1) & (NHIST - 1);
+    C.np++;
+    if (t < N) ring(S.prev, C.hp, 0, N)[t] = sm.pold[t];
+    wave_sync();
+    if (C.acceleration && (C.iter_nb == C.accel_start || C.nb_after_accel == C.accel_period)) {
+        wave_accel_step(C, S, N, sm);
+        C.nb_after_accel = 0;
+    }
+}
+
+__device__ __forceinline__ void wave_next_step_post(Ctl &C, Slot &S, int N, WaveLayer &sm, double eq) {
+    const int t = lane_id();
+    C.eq_error = eq;
+    if (C.acceleration && C.iter_nb >= C.accel_start) C.nb_after_accel++;
+    const bool better = C.eq_error < C.best_eq;
+    if (better) C.best_eq = C.eq_error;
+    C.hr = (C.hr + NHIST - 1) & (NHIST - 1);
+    C.nr++;
+    double pe = 0., re = 0.;
+    if (t < N) {
+        const double r = sm.pnew[t] - sm.pold[t];
+        ring(S.res, C.hr, 0, N)[t] = r;
+        pe = fmax(pe, fabs(r));
+        re = fmax(re, fabs(r / (sm.pold[t] + 1.e-99)));
+        if (better) S.opt[t] = sm.pold[t];
+    }
+    C.pop_error = wave_max(pe);
+    C.rel_error = wave_max(re);
+    if (C.nr > C.nb_prev + 1) C.nr = C.nb_prev + 1;
+    if (C.np > C.nb_prev + 1) C.np = C.nb_prev + 1;
+    wave_sync();
+    if (t < N) {
+        if (C.iter_nb < C.max_iter - 1) sm.pold[t] = sm.pnew[t];
+        else sm.pold[t] = S.opt[t];
+    }
+    if (C.iter_nb >= C.max_iter - 1) C.eq_error = C.best_eq;
+    C.iter_nb++;
+    wave_sync();
+}
+
+// One layer of calc_molecular_populations (radiative_transfer.cpp:236-288), one wave.
+template <int NM>
+__device__ __forceinline__ void wave_solve_layer(const LvgDevProblem &P, const LvgLaunch &Lc, const WaveShared &sh,
+                                                 WaveLayer &sm, const EscGrids &G, const int *li, int ldk, double *K,
+                                                 Slot &S, int l) {
+    const int N = P.N, t = lane_id();
+    const LvgModeLines &M = Lc.line_overlap ? P.overlap : P.plain;
+    TSTAMP(ts0);
+    if (t == 0) layer_scalars(P, Lc, l, sm);
+    wave_sync();
+    double *pops = Lc.pops + (int64_t)l * N;
+    lvg_layer_status *st = reinterpret_cast<lvg_layer_status *>(Lc.status) + l;
+    const bool need_boundary = (Lc.init != LVG_INIT_GIVEN);
+    wave_collisions(P, sh, sm, K, ldk, need_boundary ? S.A : nullptr);
+    wave_sync();
+    TACC(PH_SETUP, ts0);
+    if (!need_boundary) {
+        if (t < N) { sm.pold[t] = pops[t]; S.given[t] = pops[t]; }
+        wave_sync();
+    }
+    Ctl C;
+    const int accel = Lc.acceleration;
+    bool boundary = need_boundary, found = false;
+    int iters = 0, retry = 0;
+    const int row = t < N ? t : 0;
+    if (!boundary) wave_start_pass(C, S, Lc, N, accel ? Lc.max_iter_acc : Lc.max_iter_plain, accel);
+    for (;;) {
+        double a[NM];
+        double eq = 0.;
+        if (boundary) {
+            TSTAMP(tbd);
+            wave_boundary_rows<NM>(S.A, N, a);
+            TACC(PH_BOUNDARY, tbd);
+        } else {
+            TSTAMP(tc0);
+            wave_next_step_pre(C, S, N, sm);
+            TACC(PH_CTL, tc0);
+            TSTAMP(tl0);
+            // line terms y (compute_line_terms)
+            if (Lc.line_overlap) wave_line_terms_overlap(P, G, M, sm);
+            else wave_line_terms_plain(P, G, M, sm);
+            wave_sync();
+            TACC(PH_LINES, tl0);
+            TSTAMP(ta0);
+            // diagonal (column_diagonals): lane d folds column d of K in the reference order
+            double dg = 0.;
+            {
+                const int d = row;
+                const bool il = M.diag_interleaved != 0;
+#pragma unroll
+                for (int r = 0; r < NM; r++) {
+                    if (r < N && r != d) {
+                        dg = dg - K[r * ldk + d];
+                        if (il) {
+                            const int lv = li[r * ldk + d];
+                            if (lv >= 0) dg = dg - sm.y[lv];
+                        }
+                    }
+                }
+                if (!M.diag_interleaved)
+                    for (int q = M.diag_ptr[d]; q < M.diag_ptr[d + 1]; q++) dg = dg - sm.y[M.diag_ent[q]];
+            }
+            // row `row` of A = K + line terms, diagonal, row 0 <- 1; residual e0 - A n
+            double s = (t == 0) ? 1. : 0.;
+#pragma unroll
+            for (int j = 0; j < NM; j++) {
+                if (j < N) {
+                    double v = K[row * ldk + j];
+                    const int lv = li[row * ldk + j];
+                    if (lv >= 0) v = v + sm.y[lv];
+                    if (j == row) v = dg;
+                    if (row == 0) v = 1.;
+                    a[j] = v;
+                    s = s - v * sm.pold[j];
+                } else {
+                    a[j] = 0.;
+                }
+            }
+            eq = wave_max(t < N ? fabs(s) : 0.);
+            TACC(PH_ASSEMBLE, ta0);
+        }
+        wave_lu_solve<NM>(a, t == 0 ? 1. : 0., N, sm.pnew);
+        wave_sync();
+        if (boundary) {
+            if (t < N) { sm.pold[t] = sm.pnew[t]; S.given[t] = sm.pnew[t]; }
+            wave_sync();
+            if (Lc.dbg_mode == 2) {
+                if (t < N) pops[t] = sm.pold[t];
+                return;
+            }
+            boundary = false;
+            wave_start_pass(C, S, Lc, N, accel ? Lc.max_iter_acc : Lc.max_iter_plain, accel);
+            continue;
+        }
+        TSTAMP(tc1);
+        wave_next_step_post(C, S, N, sm, eq);
+        TACC(PH_CTL, tc1);
+        found = C.rel_error < Lc.min_error;
+        if (C.iter_nb < C.max_iter && !found) continue;
+        iters += C.iter_nb;
+        if (!retry && !found && accel && Lc.allow_plain_retry) {
+            retry = 1;
+            if (t < N) sm.pold[t] = S.given[t];
+            wave_sync();
+            wave_start_pass(C, S, Lc, N, Lc.max_iter_plain, 0);
+            continue;
+        }
+        break;
+    }
+    if (t < N) pops[t] = sm.pold[t];
+    if (t == 0) {
+        st->converged = found ? 1 : 0;
+        st->iterations = iters;
+        st->used_plain_retry = retry;
+        st->reserved = 0;
+        st->eq_error = C.eq_error;
+        st->rel_error = C.rel_error;
+        st->pop_error = C.pop_error;
+    }
+    wave_sync();
+}
+
+template <int NM>
+__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) solve_wave_kernel(const LvgDevProblem *__restrict__ Pp,
+                                                            const LvgLaunch *__restrict__ Lp) {
+    __shared__ WaveShared sh;
+    const LvgDevProblem &P = *Pp;
+    const LvgLaunch &Lc = *Lp;
+    const int N = P.N, ldk = N | 1, wpb = blockDim.x >> 6, w = threadIdx.x >> 6, tid = threadIdx.x;
+    PH_INIT();
+    const LvgModeLines &M = Lc.line_overlap ? P.overlap : P.plain;
+    int *li = reinterpret_cast<int *>(lvg_wave_dyn);
+    const int li_dbl = (N * ldk + 1) / 2;
+    double *K = lvg_wave_dyn + li_dbl + (int64_t)w * N * ldk;
+    // block-wide tables: molecule rule, escape/overlap grids, line index map
+    for (int e = tid; e < LVG_MAX_CLASSES * LVG_MAX_TERMS; e += blockDim.x) {
+        (&sh.ttab[0][0])[e] = (&P.terms.table[0][0])[e];
+        (&sh.tcombo[0][0])[e] = (&P.terms.combo[0][0])[e];
+    }
+    for (int e = tid; e < LVG_MAX_CLASSES; e += blockDim.x) {
+        sh.tet[e] = P.terms.etable[e];
+        sh.tgrp[e] = P.terms.group[e];
+    }
+    const int o1 = P.esc_nd, o2 = o1 + P.esc_ng;
+    const bool ov = Lc.line_overlap != 0;
+    const int o3 = o2 + (ov ? P.ov_nd : 0), o4 = o3 + (ov ? P.ov_ndx : 0), o5 = o4 + (ov ? P.ov_ngr : 0),
+              o6 = o5 + (ov ? P.ov_ng : 0);
+    for (int e = tid; e < o6; e += blockDim.x) {
+        double v;
+        if (e < o1) v = P.esc_delta[e];
+        else if (e < o2) v = P.esc_gamma[e - o1];
+        else if (e < o3) v = P.ov_ld[e - o2];
+        else if (e < o4) v = P.ov_dx[e - o3];
+        else if (e < o5) v = P.ov_gr[e - o4];
+        else v = P.ov_g[e - o5];
+        sh.grids[e] = v;
+    }
+    for (int e = tid; e < N * N; e += blockDim.x) {
+        const int r = e / N, d = e - r * N;
+        li[r * ldk + d] = M.line_idx[e];
+    }
+    __syncthreads();
+    const EscGrids G{sh.grids, sh.grids + o1, sh.grids + o2, sh.grids + o3, sh.grids + o4, sh.grids + o5};
+    WaveLayer &sm = sh.w[w];
+    Slot S = make_slot(P, Lc, blockIdx.x * wpb + w);
+    for (;;) {
+        int q = 0;
+        if (lane_id() == 0) q = atomicAdd(Lc.counter, 1);
+        q = __builtin_amdgcn_readfirstlane(q);
+        if (q >= Lc.nb_lay) break;
+        const int l = Lc.order ? Lc.order[q] : q;
+        wave_solve_layer<NM>(P, Lc, sh, sm, G, li, ldk, K, S, l);
+    }
+    PH_FLUSH();
+}
+
+// host-side plan: waves per block and dynamic LDS bytes for N, or 0 if the wave
+// kernel does not apply (N > 64, too many line terms or grid points for LDS)
+inline size_t wave_dyn_bytes(int N, int wpb) {
+    const int ldk = N | 1;
+    return sizeof(double) * ((size_t)(N * ldk + 1) / 2 + (size_t)wpb * N * ldk);
+}
