@@ -76,12 +76,26 @@ constexpr double MIN_LINE_OPACITY      = 1.e-99;
 #ifndef LVG_GEMM_PIPE
 #define LVG_GEMM_PIPE 1
 #endif
-constexpr int YCAP = 2048;            // line terms kept in LDS when 2*nb_lines <= YCAP
+#ifndef LVG_PANEL_W1
+#define LVG_PANEL_W1 0
+#endif
+#ifndef LVG_PANEL_PRIO
+#define LVG_PANEL_PRIO 0
+#endif
+#ifndef LVG_OCC
+#define LVG_OCC 2                     // resident workgroups per CU solve_kernel is built for
+#endif
+constexpr int YCAP = (LVG_OCC >= 3) ? 1 : 2048;   // line terms kept in LDS when 2*nb_lines <= YCAP
 constexpr int TC = 4;                 // columns per thread in the LU register tile (8 rows x TC)
 constexpr int WB = 8 * TC;            // LU block-column width
 
 struct Smem {
-    double pold[NMAX], pnew[NMAX], bvec[NMAX], blog[NMAX];
+    double pold[NMAX], bvec[NMAX];
+#if LVG_OCC >= 3
+    union { double pnew[NMAX]; double blog[NMAX]; };   // pnew only ever copies blog
+#else
+    double pnew[NMAX], blog[NMAX];
+#endif
     double diag[NMAX];          // assembled diagonal of the rate matrix (fused assembly)
     double ylds[YCAP];          // line terms y of the current iteration (if they fit)
     int    perm[NMAX];          // LU row permutation: logical position -> physical row
@@ -96,6 +110,7 @@ struct Smem {
     union alignas(16) {
         double P[NMAX][NB + 1]; // panel, physical rows
         double LT[NB][NMAX];    // L of one chunk, transposed, physical rows
+        double hist_acc[32];    // accel_step sums (used outside the LU only)
     } pu;
     // per-layer scalars
     double T, Te, vw, vgrad, nmol, ne;
@@ -110,7 +125,6 @@ struct Smem {
     int8_t ttab[LVG_MAX_CLASSES][LVG_MAX_TERMS], tcombo[LVG_MAX_CLASSES][LVG_MAX_TERMS];
     int8_t tet[LVG_MAX_CLASSES], tgrp[LVG_MAX_CLASSES];
     double dust[LVG_MAX_DUST];
-    double hist_acc[32];
     int    layer, pidx;
 };
 
@@ -654,6 +668,7 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
     // right-hand side b[p] in a register; the pivot candidate of each wave publishes
     // its row and its b through LDS.
     const int t = threadIdx.x, w = t >> 6;
+    if (LVG_PANEL_PRIO) __builtin_amdgcn_s_setprio(2);
     double rw[NB];
     const bool valid = t < N;
     const int p = valid ? t : 0;
@@ -746,8 +761,118 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
 #pragma unroll
         for (int j = 0; j < NB; j++) sm.pu.P[p][j] = rw[j];
     }
+    if (LVG_PANEL_PRIO) __builtin_amdgcn_s_setprio(0);
     __syncthreads();
     TACC(PH_P_WB, tpw);
+}
+
+// Single-wave panel (LVG_PANEL_W1): wave 0 factors the chunk alone, NMAX/64 rows per
+// lane in registers (physical rows ln, ln+64, ...). Per column: a compare over the
+// lane's rows, one DPP wave reduction (+ ballot) for the pivot and a v_readlane
+// broadcast of the pivot row; no workgroup barrier and no LDS round trip. Same
+// pivots (largest |v|, ties to the smallest logical position) and the same fma
+// sequence as panel_factor, so the factors are identical. Waves 1-3 go straight to
+// the closing barrier and leave their SIMDs to the co-resident workgroup.
+__device__ __forceinline__ void panel_factor_w1(double *A, int N, int kk, int nb, double *b, Smem &sm) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) < 64) {
+        if (LVG_PANEL_PRIO) __builtin_amdgcn_s_setprio(2);
+        constexpr int R = NMAX / 64;
+        static_assert(R == 4, "four rows per lane");
+        const int ln = threadIdx.x;
+        double rw[R][NB], rb[R];
+        bool act[R], part[R];
+        int lp[R];
+#pragma unroll
+        for (int i = 0; i < R; i++) {
+            const int p = ln + 64 * i;
+            const int pp = p < N ? p : 0;
+            const int ps = sm.pos[pp];
+            part[i] = p < N && ps >= kk;
+            act[i] = part[i];
+            lp[i] = part[i] ? ps - kk : 0x7fffffff;
+            rb[i] = b[pp];
+#pragma unroll
+            for (int j = 0; j < NB; j++) rw[i][j] = sm.pu.P[pp][j];
+        }
+#pragma clang loop unroll(full)
+        for (int c = 0; c < NB; c++) {
+            if (c < nb) {
+                // the lane's best row: largest |v| (bit pattern; active rows flagged in
+                // the top bit), ties to the smallest logical position
+                unsigned bh = 0u, bl = 0u;
+                int bp = 0x7fffffff, bs = 0;
+#pragma unroll
+                for (int i = 0; i < R; i++) {
+                    const double av = fabs(rw[i][c]);
+                    const unsigned long long bits =
+                        (act[i] && av == av) ? (unsigned long long)__double_as_longlong(av) : 0ull;
+                    const unsigned hi = act[i] ? ((unsigned)(bits >> 32) | 0x80000000u) : 0u, lo = (unsigned)bits;
+                    const bool better = hi > bh || (hi == bh && (lo > bl || (lo == bl && (unsigned)lp[i] < (unsigned)bp)));
+                    bh = better ? hi : bh;
+                    bl = better ? lo : bl;
+                    bp = better ? lp[i] : bp;
+                    bs = better ? i : bs;
+                }
+                const unsigned H = wave_max_u32(bh);
+                const unsigned long long tie = __ballot(bh == H);
+                int pl;
+                if (__popcll(tie) == 1) {
+                    pl = __ffsll((long long)tie) - 1;
+                } else {
+                    const unsigned Lw = wave_max_u32(bh == H ? bl : 0u);
+                    const unsigned X = wave_max_u32((bh == H && bl == Lw) ? ~(unsigned)bp : 0u);
+                    pl = __ffsll((long long)__ballot(bh == H && bl == Lw && bp == (int)~X)) - 1;
+                }
+                pl = __builtin_amdgcn_readfirstlane(pl);
+                const int s = __builtin_amdgcn_readlane(bs, pl);
+                const int plp = __builtin_amdgcn_readlane(bp, pl);
+                double prow[NB], bc;
+                auto bcast = [&](const double (&r)[NB], double rbv) {
+#pragma unroll
+                    for (int j = 0; j < NB; j++) if (j >= c) prow[j] = readlane_d(r[j], pl);
+                    bc = readlane_d(rbv, pl);
+                };
+                if (s == 0) bcast(rw[0], rb[0]);
+                else if (s == 1) bcast(rw[1], rb[1]);
+                else if (s == 2) bcast(rw[2], rb[2]);
+                else bcast(rw[3], rb[3]);
+                const double piv = prow[c];
+#pragma unroll
+                for (int i = 0; i < R; i++) {
+                    if (ln == pl && s == i) { act[i] = false; lp[i] = c; }
+                    else if (lp[i] == c) lp[i] = plp;
+                    if (act[i]) {
+                        const double l = rw[i][c] / piv;
+                        rw[i][c] = l;
+#pragma unroll
+                        for (int j = 0; j < NB; j++) if (j > c) rw[i][j] = fma(-l, prow[j], rw[i][j]);
+                        rb[i] = fma(-l, bc, rb[i]);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < R; i++) {
+            if (part[i]) {
+                const int p = ln + 64 * i;
+                if ((N & 1) == 0 && nb == NB) {
+                    double2 *d2 = reinterpret_cast<double2 *>(A + (int64_t)p * N + kk);
+#pragma unroll
+                    for (int j = 0; j < NB / 2; j++) d2[j] = make_double2(rw[i][2 * j], rw[i][2 * j + 1]);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < NB; j++) if (j < nb) A[(int64_t)p * N + kk + j] = rw[i][j];
+                }
+                sm.perm[kk + lp[i]] = p;
+                sm.pos[p] = kk + lp[i];
+                b[p] = rb[i];
+#pragma unroll
+                for (int j = 0; j < NB; j++) sm.pu.P[p][j] = rw[i][j];
+            }
+        }
+        if (LVG_PANEL_PRIO) __builtin_amdgcn_s_setprio(0);
+    }
+    __syncthreads();
 }
 
 __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Smem &sm, const LuSrc &src, const bool FUSED) {
@@ -894,7 +1019,8 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                     }
                 }
                 __syncthreads();
-                panel_factor(A, N, kk, nb, b, sm);
+                if (LVG_PANEL_W1) panel_factor_w1(A, N, kk, nb, b, sm);
+                else panel_factor(A, N, kk, nb, b, sm);
                 for (int e = t; e < NB * NB; e += BT) {
                     const int r = e / NB, m = e - r * NB;
                     sm.L11[r][m] = (r < nb && m < r) ? sm.pu.P[sm.perm[kk + r]][m] : 0.;
@@ -931,11 +1057,13 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                 for (int m = 0; m < NB; m++) lrow[m] = (la && m < nb) ? sm.pu.P[la ? trow : 0][m] : 0.;
             }
             // ---- pivot rows of chunk kk (logical kk..kk+nb-1): their current values
-            //      in this block column -> Ub (owners write from registers)
+            //      in this block column -> Ub (owners write from registers). For an
+            //      earlier block's chunk they are tile rows kk.. (logical order as of
+            //      the block load, when those pivots were already final).
 #pragma unroll
             for (int i = 0; i < 8; i++) {
                 if (8 * rg + i < N) {
-                    const int q = sm.pos[prow[i]] - kk;
+                    const int q = (kk < c0 ? 8 * rg + i : sm.pos[prow[i]]) - kk;
                     if (q >= 0 && q < nb) {
 #pragma unroll
                         for (int j = 0; j < TC; j++) sm.Ub[q][TC * cg + j] = acc[i][j];
@@ -1163,14 +1291,14 @@ __device__ __forceinline__ void accel_step(Ctl &C, Slot &S, int N, Smem &sm) {
             double num = (j >= 0) ? (r0[k] - ri[k]) * (r0[k] - rj[k]) : (r0[k] - ri[k]) * r0[k];
             a = a + num / (w * w);
         }
-        sm.hist_acc[t] = a;
+        sm.pu.hist_acc[t] = a;
     }
     __syncthreads();
     if (t == 0) {
         double Am[4][4], bv[4];
         for (int i = 0; i < np; i++) {
-            for (int j = 0; j < np; j++) Am[i][j] = sm.hist_acc[i * np + j];
-            bv[i] = sm.hist_acc[np * np + i];
+            for (int j = 0; j < np; j++) Am[i][j] = sm.pu.hist_acc[i * np + j];
+            bv[i] = sm.pu.hist_acc[np * np + i];
         }
         for (int k = 0; k < np; k++) {
             int p = k;
@@ -1194,14 +1322,14 @@ __device__ __forceinline__ void accel_step(Ctl &C, Slot &S, int N, Smem &sm) {
             for (int i = 0; i < k; i++) bv[i] = fma(-Am[i][k], x, bv[i]);
         }
         double sum = 0.;
-        for (int i = 0; i < np; i++) { sum = sum + bv[i]; sm.hist_acc[16 + i] = bv[i]; }
-        sm.hist_acc[31] = sum;
+        for (int i = 0; i < np; i++) { sum = sum + bv[i]; sm.pu.hist_acc[16 + i] = bv[i]; }
+        sm.pu.hist_acc[31] = sum;
     }
     __syncthreads();
-    const double sum = sm.hist_acc[31];
+    const double sum = sm.pu.hist_acc[31];
     for (int k = t; k < N; k += BT) {
         double a = (1. - sum) * p0[k];
-        for (int i = 0; i < np; i++) a = a + sm.hist_acc[16 + i] * ring(S.prev, C.hp, i + 1, N)[k];
+        for (int i = 0; i < np; i++) a = a + sm.pu.hist_acc[16 + i] * ring(S.prev, C.hp, i + 1, N)[k];
         sm.pold[k] = a;
     }
     __syncthreads();
@@ -1391,7 +1519,7 @@ __device__ __forceinline__ void solve_layer(const LvgDevProblem &P, const LvgLau
     __syncthreads();
 }
 
-__global__ void __launch_bounds__(BT, 2) solve_kernel(const LvgDevProblem *__restrict__ Pp,
+__global__ void __launch_bounds__(BT, LVG_OCC) solve_kernel(const LvgDevProblem *__restrict__ Pp,
                                                        const LvgLaunch *__restrict__ Lp) {
     __shared__ Smem sm;
     const LvgDevProblem &P = *Pp;
