@@ -82,6 +82,12 @@ constexpr double MIN_LINE_OPACITY      = 1.e-99;
 #ifndef LVG_PANEL_PRIO
 #define LVG_PANEL_PRIO 0
 #endif
+#ifndef LVG_L11_ROWS
+#define LVG_L11_ROWS 0
+#endif
+#ifndef LVG_LA_TILE
+#define LVG_LA_TILE 1
+#endif
 #ifndef LVG_OCC
 #define LVG_OCC 2                     // resident workgroups per CU solve_kernel is built for
 #endif
@@ -986,7 +992,12 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
         bool have_next = false;
         auto fetch_l = [&](int k2, double (&lr)[NB], double &l11) {
             const int nb2 = min(NB, N - k2);
-            const bool la = t < N && sm.pos[trow] >= k2 + nb2;
+            // tile row t is logical row t here (earlier pivots were final at the block
+            // load), so rows t >= k2 + nb2 are below the chunk (LVG_LA_TILE: no LDS
+            // lookup) and rows k2..k2+nb2-1 are its pivot rows, whose L part is L11
+            // (LVG_L11_ROWS: L11 from those rows instead of a separate load)
+            const bool la = LVG_L11_ROWS ? (t < N && t >= k2)
+                          : LVG_LA_TILE ? (t < N && t >= k2 + nb2) : (t < N && sm.pos[trow] >= k2 + nb2);
             const double *src_l = A + (int64_t)(la ? trow : 0) * N + k2;
             if ((N & 1) == 0 && nb2 == NB) {
                 // 16-byte aligned row segment (N even, k2 a multiple of 16): 8 vector loads
@@ -1001,8 +1012,11 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
 #pragma unroll
                 for (int m = 0; m < NB; m++) lr[m] = (la && m < nb2) ? src_l[m] : 0.;
             }
-            const int r = t / NB, m = t - r * NB;
-            l11 = (t < NB * NB && r < nb2 && m < r) ? A[(int64_t)sm.perm[k2 + r] * N + k2 + m] : 0.;
+            l11 = 0.;
+            if (!LVG_L11_ROWS) {
+                const int r = t / NB, m = t - r * NB;
+                l11 = (t < NB * NB && r < nb2 && m < r) ? A[(int64_t)sm.perm[k2 + r] * N + k2 + m] : 0.;
+            }
         };
         for (int kk = 0; kk < c0 + wJ; kk += NB) {
             const int nb = min(NB, N - kk);
@@ -1070,7 +1084,17 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                     }
                 }
             }
-            if (kk < c0 && t < NB * NB) sm.L11[t / NB][t % NB] = l11v;
+            if (kk < c0) {
+                if (LVG_L11_ROWS) {
+                    if (t >= kk && t < kk + NB) {      // pivot row t - kk: its L part -> L11, stages l = 0
+                        const int r = t - kk;
+#pragma unroll
+                        for (int m = 0; m < NB; m++) { sm.L11[r][m] = (m < r) ? lrow[m] : 0.; lrow[m] = 0.; }
+                    }
+                } else if (t < NB * NB) {
+                    sm.L11[t / NB][t % NB] = l11v;
+                }
+            }
             __syncthreads();
             TACC(PH_T_FETCH, tp2);
             TSTAMP(tp2s);
