@@ -74,7 +74,7 @@ constexpr double MIN_LINE_OPACITY      = 1.e-99;
 #define LVG_PREFETCH_L 0
 #endif
 #ifndef LVG_GEMM_PIPE
-#define LVG_GEMM_PIPE 1
+#define LVG_GEMM_PIPE 0
 #endif
 #ifndef LVG_PANEL_W1
 #define LVG_PANEL_W1 0
