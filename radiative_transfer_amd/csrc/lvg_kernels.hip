@@ -88,6 +88,9 @@ constexpr double MIN_LINE_OPACITY      = 1.e-99;
 #ifndef LVG_LA_TILE
 #define LVG_LA_TILE 1
 #endif
+#ifndef LVG_PANEL_ONEWAVE
+#define LVG_PANEL_ONEWAVE 1
+#endif
 #ifndef LVG_OCC
 #define LVG_OCC 2                     // resident workgroups per CU solve_kernel is built for
 #endif
@@ -779,21 +782,25 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
 // pivots (largest |v|, ties to the smallest logical position) and the same fma
 // sequence as panel_factor, so the factors are identical. Waves 1-3 go straight to
 // the closing barrier and leave their SIMDs to the co-resident workgroup.
-__device__ __forceinline__ void panel_factor_w1(double *A, int N, int kk, int nb, double *b, Smem &sm) {
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x) < 64) {
+// R = 1 (the product path): when every row still active in the chunk lies in one
+// wave's tile rows (block columns c0 >= 64 * ((N - 1) / 64)), that wave factors the
+// chunk alone with its own rows. R = 4 (LVG_PANEL_W1, measured slower: the rows spill)
+// covers all rows from wave 0.
+template <int R>
+__device__ __forceinline__ void panel_factor_wave(double *A, int N, int kk, int nb, double *b, Smem &sm, int w0,
+                                                  const int (&rows)[R]) {
+    if ((__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6) == w0) {
         if (LVG_PANEL_PRIO) __builtin_amdgcn_s_setprio(2);
-        constexpr int R = NMAX / 64;
-        static_assert(R == 4, "four rows per lane");
-        const int ln = threadIdx.x;
+        const int ln = threadIdx.x & 63;
         double rw[R][NB], rb[R];
         bool act[R], part[R];
         int lp[R];
 #pragma unroll
         for (int i = 0; i < R; i++) {
-            const int p = ln + 64 * i;
-            const int pp = p < N ? p : 0;
+            const int p = rows[i];
+            const int pp = p >= 0 ? p : 0;
             const int ps = sm.pos[pp];
-            part[i] = p < N && ps >= kk;
+            part[i] = p >= 0 && ps >= kk;
             act[i] = part[i];
             lp[i] = part[i] ? ps - kk : 0x7fffffff;
             rb[i] = b[pp];
@@ -838,10 +845,10 @@ __device__ __forceinline__ void panel_factor_w1(double *A, int N, int kk, int nb
                     for (int j = 0; j < NB; j++) if (j >= c) prow[j] = readlane_d(r[j], pl);
                     bc = readlane_d(rbv, pl);
                 };
-                if (s == 0) bcast(rw[0], rb[0]);
-                else if (s == 1) bcast(rw[1], rb[1]);
-                else if (s == 2) bcast(rw[2], rb[2]);
-                else bcast(rw[3], rb[3]);
+                if (R == 1 || s == 0) bcast(rw[0], rb[0]);
+                else if (R == 2 || s == 1) bcast(rw[R > 1 ? 1 : 0], rb[R > 1 ? 1 : 0]);
+                else if (R == 3 || s == 2) bcast(rw[R > 2 ? 2 : 0], rb[R > 2 ? 2 : 0]);
+                else bcast(rw[R > 3 ? 3 : 0], rb[R > 3 ? 3 : 0]);
                 const double piv = prow[c];
 #pragma unroll
                 for (int i = 0; i < R; i++) {
@@ -860,7 +867,7 @@ __device__ __forceinline__ void panel_factor_w1(double *A, int N, int kk, int nb
 #pragma unroll
         for (int i = 0; i < R; i++) {
             if (part[i]) {
-                const int p = ln + 64 * i;
+                const int p = rows[i];
                 if ((N & 1) == 0 && nb == NB) {
                     double2 *d2 = reinterpret_cast<double2 *>(A + (int64_t)p * N + kk);
 #pragma unroll
@@ -1033,8 +1040,17 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                     }
                 }
                 __syncthreads();
-                if (LVG_PANEL_W1) panel_factor_w1(A, N, kk, nb, b, sm);
-                else panel_factor(A, N, kk, nb, b, sm);
+                if (LVG_PANEL_W1) {
+                    const int r4[4] = {t < N ? t : -1, t + 64 < N ? t + 64 : -1, t + 128 < N ? t + 128 : -1,
+                                       t + 192 < N ? t + 192 : -1};
+                    panel_factor_wave<4>(A, N, kk, nb, b, sm, 0, r4);
+                } else if (LVG_PANEL_ONEWAVE && (c0 >> 6) == ((N - 1) >> 6)) {
+                    // every active row is a tile row >= c0, all in wave c0 / 64: no barriers
+                    const int r1[1] = {t < N ? trow : -1};
+                    panel_factor_wave<1>(A, N, kk, nb, b, sm, c0 >> 6, r1);
+                } else {
+                    panel_factor(A, N, kk, nb, b, sm);
+                }
                 for (int e = t; e < NB * NB; e += BT) {
                     const int r = e / NB, m = e - r * NB;
                     sm.L11[r][m] = (r < nb && m < r) ? sm.pu.P[sm.perm[kk + r]][m] : 0.;
