@@ -89,7 +89,7 @@ constexpr double MIN_LINE_OPACITY      = 1.e-99;
 #define LVG_LA_TILE 1
 #endif
 #ifndef LVG_PANEL_ONEWAVE
-#define LVG_PANEL_ONEWAVE 1
+#define LVG_PANEL_ONEWAVE 2
 #endif
 #ifndef LVG_OCC
 #define LVG_OCC 2                     // resident workgroups per CU solve_kernel is built for
@@ -107,6 +107,7 @@ struct Smem {
 #endif
     double diag[NMAX];          // assembled diagonal of the rate matrix (fused assembly)
     double ylds[YCAP];          // line terms y of the current iteration (if they fit)
+    int    tmap[NMAX];          // physical row of each tile row at the current block load
     int    perm[NMAX];          // LU row permutation: logical position -> physical row
     int    pos[NMAX];           // its inverse: physical row -> logical position
     double red[8];
@@ -912,6 +913,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
 #pragma unroll
         for (int i = 0; i < 8; i++) prow[i] = (8 * rg + i < N) ? sm.perm[8 * rg + i] : 0;
         const int trow = (t < N) ? sm.perm[t] : 0;   // physical row of tile row t (L staging)
+        if (LVG_PANEL_ONEWAVE >= 2 && t < N) sm.tmap[t] = trow;
         if (LVG_L2_PREFETCH) {
             l2_token_use(pf_blk0); l2_token_use(pf_blk1); l2_token_use(pf_blk2); l2_token_use(pf_l);
             if (c0 > 0) pf_l = l2_token(A + (int64_t)trow * N);                    // L of chunk 0
@@ -1044,6 +1046,17 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                     const int r4[4] = {t < N ? t : -1, t + 64 < N ? t + 64 : -1, t + 128 < N ? t + 128 : -1,
                                        t + 192 < N ? t + 192 : -1};
                     panel_factor_wave<4>(A, N, kk, nb, b, sm, 0, r4);
+                } else if (LVG_PANEL_ONEWAVE >= 3 && c0 >= 64 && (c0 >> 7) != ((N - 1) >> 7) && ((N - 1) >> 6) == 3) {
+                    // active rows in tile rows 64..255: one wave takes three rows per lane
+                    const int l = t & 63;
+                    const int r3[3] = {64 + l < N ? sm.tmap[64 + l] : -1, 128 + l < N ? sm.tmap[128 + l] : -1,
+                                       192 + l < N ? sm.tmap[192 + l] : -1};
+                    panel_factor_wave<3>(A, N, kk, nb, b, sm, 1, r3);
+                } else if (LVG_PANEL_ONEWAVE >= 2 && (c0 >> 6) != ((N - 1) >> 6) && (c0 >> 7) == ((N - 1) >> 7)) {
+                    // active rows within two waves' tile rows: one wave takes both (2 rows per lane)
+                    const int base = (c0 >> 7) << 7, l = t & 63;
+                    const int r2[2] = {base + l < N ? sm.tmap[base + l] : -1, base + 64 + l < N ? sm.tmap[base + 64 + l] : -1};
+                    panel_factor_wave<2>(A, N, kk, nb, b, sm, base >> 6, r2);
                 } else if (LVG_PANEL_ONEWAVE && (c0 >> 6) == ((N - 1) >> 6)) {
                     // every active row is a tile row >= c0, all in wave c0 / 64: no barriers
                     const int r1[1] = {t < N ? trow : -1};
