@@ -24,6 +24,15 @@
  * multiply-add (fma) — the absent library's rounding is unknown anyway; exp and
  * log10 come from include/lvg_math.h (< 1-2 ulp from libm, identical on host and
  * device); the thermal width uses sqrt(x) for the reference's pow(x, 0.5).
+ *
+ * ORACLE_REF_ARITH (second build, oracle/_build/liblvg_oracle_ref.so): the same
+ * restatement with the reference's own arithmetic instead of those three choices —
+ * glibc exp/log10/log (coll_rates.cpp:194, coll_rates_ch3oh.cpp:531,
+ * transition_data.cpp:348, lvg_method_functions.cpp:330), pow(x, 0.5) and pow(x, 2.)
+ * (iteration_lvg.cpp:65, transition_data.cpp:256-262), and an LU whose updates are
+ * a - l*b with two roundings (no FMA; lu_matrix_solve call site iteration_lvg.cpp:100).
+ * tests/test_oracle_refarith_cpu.py measures how far the bit-exact build sits from
+ * it against SURVEY.md 8(c)'s tolerances.
  */
 #include "lvg_oracle.h"
 #include "../include/lvg_math.h"
@@ -34,6 +43,30 @@
 #ifdef _OPENMP
 #include <omp.h>
 #endif
+
+#ifdef ORACLE_REF_ARITH
+#define O_EXP(x)         exp(x)
+#define O_LOG10(x)       log10(x)
+#define O_LOG(x)         log(x)
+#define O_FMSUB(l, b, a) ((a) - (l) * (b))      /* a -= l*b: product and difference rounded */
+#define O_SQRT(x)        pow((x), 0.5)
+#define O_SQR(x)         pow((x), 2.)
+#else
+#define O_EXP(x)         lvg_exp(x)
+#define O_LOG10(x)       lvg_log10(x)
+#define O_LOG(x)         lvg_log(x)
+#define O_FMSUB(l, b, a) fma(-(l), (b), (a))
+#define O_SQRT(x)        sqrt(x)
+#define O_SQR(x)         ((x) * (x))
+#endif
+int oracle_ref_arith(void)
+{
+#ifdef ORACLE_REF_ARITH
+    return 1;
+#else
+    return 0;
+#endif
+}
 
 /* constants.h (absent; CODATA 2018, CGS) — used at iteration_lvg.cpp:65, :168,
  * :455, coll_rates.cpp:194 */
@@ -89,15 +122,15 @@ int oracle_lu_solve(double *a, double *b, int n)
             double l = a[i * n + k] / piv;
             a[i * n + k] = l;
             for (int j = k + 1; j < n; j++)
-                a[i * n + j] = fma(-l, a[k * n + j], a[i * n + j]);
-            b[i] = fma(-l, b[k], b[i]);
+                a[i * n + j] = O_FMSUB(l, a[k * n + j], a[i * n + j]);
+            b[i] = O_FMSUB(l, b[k], b[i]);
         }
     }
     for (int k = n - 1; k >= 0; k--) {
         b[k] /= a[k * n + k];
         double x = b[k];
         for (int i = 0; i < k; i++)
-            b[i] = fma(-a[i * n + k], x, b[i]);
+            b[i] = O_FMSUB(a[i * n + k], x, b[i]);
     }
     return sing ? -1 : 0;
 }
@@ -155,7 +188,7 @@ double oracle_overlap_esc_func(const lvg_overlap_table *T, double gamma, double 
 {
     int l, k, n, m;
     double u, t, p, y, escf;
-    delta = lvg_log10(delta);
+    delta = O_LOG10(delta);
     m = locate_index(T->log10_delta, T->nb_d, delta);
     l = locate_index(T->gamma, T->nb_g, gamma);
     k = locate_index(T->gratio, T->nb_gr, gamma_ratio);
@@ -291,7 +324,7 @@ static void get_rate_neutrals(const scheme_t *S, int up, int low, double *down_r
             d = KRATE(0, tn) * (c[0] + c[1] + 3. * c[2]);
         }
         if (d > MIN_COLLISION_RATE)
-            *up_rate = d * lvg_exp((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / tn) * M->g[up] / ((double)M->g[low]);
+            *up_rate = d * O_EXP((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / tn) * M->g[up] / ((double)M->g[low]);
         else *up_rate = d = 0.;
         *down_rate = d;
         return;
@@ -302,7 +335,7 @@ static void get_rate_neutrals(const scheme_t *S, int up, int low, double *down_r
         else
             d = KRATE(1, tn) * c[1] + KRATE(4, tn) * c[4];
         if (d > MIN_COLLISION_RATE)
-            *up_rate = d * lvg_exp((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / tn) * M->g[up] / ((double)M->g[low]);
+            *up_rate = d * O_EXP((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / tn) * M->g[up] / ((double)M->g[low]);
         else *up_rate = d = 0.;
         *down_rate = d;
         return;
@@ -317,7 +350,7 @@ static void get_rate_neutrals(const scheme_t *S, int up, int low, double *down_r
         if (up < tab[1].nb_lev)
             d += KRATE(1, tn) * c[1] + KRATE(2, tn) * c[2];
         if (d > MIN_COLLISION_RATE)
-            u = d * lvg_exp((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / tn) * M->g[up] / ((double)M->g[low]);
+            u = d * O_EXP((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / tn) * M->g[up] / ((double)M->g[low]);
         else d = 0.;
         *down_rate = d; *up_rate = u;
         return;
@@ -326,7 +359,7 @@ static void get_rate_neutrals(const scheme_t *S, int up, int low, double *down_r
     for (int i = 0; i < C->nb_neutral; i++)
         if (up < tab[i].nb_lev) d += KRATE(i, tn) * c[i];
     if (d > MIN_COLLISION_RATE)
-        *up_rate = d * lvg_exp((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / tn) * M->g[up] / ((double)M->g[low]);
+        *up_rate = d * O_EXP((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / tn) * M->g[up] / ((double)M->g[low]);
     else *up_rate = d = 0.;
     *down_rate = d;
 }
@@ -343,7 +376,7 @@ static void get_rate_electrons(const scheme_t *S, int up, int low, double *down_
         if (up < tab[i].nb_lev) { d = KRATE(i, te) * S->conc[i]; break; }
     }
     if (d > MIN_COLLISION_RATE)
-        *up_rate = d * lvg_exp((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / te) * M->g[up] / ((double)M->g[low]);
+        *up_rate = d * O_EXP((M->energy[low] - M->energy[up]) * CM_INVERSE_TO_KELVINS / te) * M->g[up] / ((double)M->g[low]);
     else *up_rate = d = 0.;
     *down_rate = d;
 }
@@ -365,7 +398,7 @@ static void scheme_set_layer(scheme_t *S, const lvg_layers *L, int l)
     S->temp_n = LAYER(temp_n);
     S->temp_el = LAYER(temp_el);
     S->mol_conc = LAYER(mol_conc);
-    S->vel_width = sqrt(2. * BOLTZMANN_CONSTANT * S->temp_n / S->P->mol->mass + LAYER(vel_turb) * LAYER(vel_turb));
+    S->vel_width = O_SQRT(2. * BOLTZMANN_CONSTANT * S->temp_n / S->P->mol->mass + LAYER(vel_turb) * LAYER(vel_turb));
     set_gas_param(S, LAYER(temp_n), LAYER(temp_el), LAYER(he_conc), LAYER(ph2_conc), LAYER(oh2_conc),
                   LAYER(h_conc), LAYER(el_conc));
 }
@@ -1009,7 +1042,7 @@ static void o_calc_exc_temp(otrans_t *t, const lvg_problem *P, int nlay, const d
     for (int lay = 0; lay < nlay; lay++) {
         double low_pop = pop[lay * N + t->low], up_pop = pop[lay * N + t->up];
         t->exc_temp_arr[lay] = CM_INVERSE_TO_KELVINS * t->energy
-            / lvg_log((low_pop * P->mol->g[t->up]) / (up_pop * P->mol->g[t->low]));
+            / O_LOG((low_pop * P->mol->g[t->up]) / (up_pop * P->mol->g[t->low]));
     }
 }
 
@@ -1024,10 +1057,10 @@ static void o_calc_gain(otrans_t *t, const lvg_problem *P, const lvg_layers *L, 
     for (int lay = 0; lay < nlay; lay++) {
         double vel, vt = L->vel_turb[lay];
         if (h2o22) {
-            double a = sqrt(2. * BOLTZMANN_CONSTANT * L->temp_n[lay] / P->mol->mass) + 5.e+4;
-            vel = sqrt(a * a + vt * vt);
+            double a = O_SQRT(2. * BOLTZMANN_CONSTANT * L->temp_n[lay] / P->mol->mass) + 5.e+4;
+            vel = O_SQRT(a * a + vt * vt);
         } else {
-            vel = sqrt(2. * BOLTZMANN_CONSTANT * L->temp_n[lay] / P->mol->mass + vt * vt);
+            vel = O_SQRT(2. * BOLTZMANN_CONSTANT * L->temp_n[lay] / P->mol->mass + vt * vt);
         }
         double line_gain = t->inv_arr[lay] * P->mol->g[t->up] * aul * ONEDIVBY_SQRT_PI * L->mol_conc[lay]
             / (energy_th * EIGHT_PI * vel);
@@ -1059,7 +1092,7 @@ static void o_calc_line_profile(otrans_t *t, const lvg_problem *P, const lvg_lay
     double *od = (double *)malloc(sizeof(double) * LVG_NB_FREQ * LVG_NB_ASPECT);
     for (int lay = 0; lay < nlay; lay++) {
         double vt = L->vel_turb[lay];
-        vw[lay] = sqrt(2. * BOLTZMANN_CONSTANT * L->temp_n[lay] / P->mol->mass + vt * vt);
+        vw[lay] = O_SQRT(2. * BOLTZMANN_CONSTANT * L->temp_n[lay] / P->mol->mass + vt * vt);
         lo[lay] = t->inv_arr[lay] * P->mol->g[t->up] * aul * L->mol_conc[lay] * ONEDIVBY_SQRT_PI
             / (energy_th * EIGHT_PI * vw[lay]);
         dop[lay] = nc ? oracle_dust_absorption(P->dust, energy, L->dust_conc + (size_t)lay * nc) : 0.;
@@ -1071,7 +1104,7 @@ static void o_calc_line_profile(otrans_t *t, const lvg_problem *P, const lvg_lay
             double acc = 0.;
             for (int lay = 0; lay < nlay; lay++) {
                 double x = (vel - G->vel_n[lay] / aspect_ratio) / vw[lay];
-                double profile = lvg_exp(-x * x);
+                double profile = O_EXP(-x * x);
                 if (lo[lay] * profile - dop[lay] > 0.)
                     acc += (lo[lay] * profile - dop[lay]) * G->dz[lay] * aspect_ratio;
             }

@@ -16,13 +16,15 @@ from radiative_transfer_amd import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "liblvg_oracle.so")
-_lib = None
+# reference-arithmetic build (-DORACLE_REF_ARITH): glibc exp/log10/pow, LU without fma
+REF_LIB_PATH = os.path.join(HERE, "_build", "liblvg_oracle_ref.so")
+_libs = {}
 
 
 def _stale() -> bool:
-    if not os.path.exists(LIB_PATH):
+    if not (os.path.exists(LIB_PATH) and os.path.exists(REF_LIB_PATH)):
         return True
-    t = os.path.getmtime(LIB_PATH)
+    t = min(os.path.getmtime(LIB_PATH), os.path.getmtime(REF_LIB_PATH))
     deps = [os.path.join(HERE, f) for f in ("lvg_oracle.c", "lvg_oracle.h", "Makefile")]
     deps += [os.path.join(HERE, "..", "include", f) for f in ("lvg_amd.h", "lvg_math.h")]
     return any(os.path.getmtime(x) > t for x in deps)
@@ -34,11 +36,11 @@ def build(force: bool = False) -> str:
     return LIB_PATH
 
 
-def lib():
-    global _lib
-    if _lib is None:
+def lib(ref: bool = False):
+    """The bit-exact oracle, or with ref=True its reference-arithmetic build."""
+    if ref not in _libs:
         build()
-        L = C.CDLL(LIB_PATH)
+        L = C.CDLL(REF_LIB_PATH if ref else LIB_PATH)
         d, i, vp = C.c_double, C.c_int, C.c_void_p
         dp = C.POINTER(C.c_double)
         L.oracle_solve_layers.argtypes = [vp, vp, dp, vp, vp, i]
@@ -61,42 +63,44 @@ def lib():
         L.oracle_exp.restype = d
         L.oracle_log10.argtypes = [d]
         L.oracle_log10.restype = d
-        _lib = L
-    return _lib
+        L.oracle_ref_arith.restype = i
+        assert L.oracle_ref_arith() == int(ref)
+        _libs[ref] = L
+    return _libs[ref]
 
 
 def _nz(a):
     return abi.dptr(a) if a is not None else None
 
 
-def solve_layers(prob: abi.Problem, layers: abi.Layers, opts=None, pops=None, nthreads: int = 0):
+def solve_layers(prob: abi.Problem, layers: abi.Layers, opts=None, pops=None, nthreads: int = 0, ref: bool = False):
     cp, cl = prob.to_c(), layers.to_c()
     N = prob.mol.nb_lev
     o = opts if opts is not None else abi.default_opts()
     out = np.zeros((layers.nb_lay, N)) if pops is None else np.array(pops, dtype=np.float64, copy=True)
     st = np.zeros(layers.nb_lay, dtype=abi.STATUS_DTYPE)
-    rc = lib().oracle_solve_layers(cp.ptr, cl.ptr, abi.dptr(out), C.byref(o),
+    rc = lib(ref).oracle_solve_layers(cp.ptr, cl.ptr, abi.dptr(out), C.byref(o),
                                    st.ctypes.data_as(C.c_void_p), nthreads)
     if rc != 0:
         raise RuntimeError(f"oracle_solve_layers failed: {rc}")
     return out, st
 
 
-def calc_new_pop(prob, layers, layer, pop_in, overlap=0):
+def calc_new_pop(prob, layers, layer, pop_in, overlap=0, ref: bool = False):
     cp, cl = prob.to_c(), layers.to_c()
     N = prob.mol.nb_lev
     pin = np.ascontiguousarray(pop_in, dtype=np.float64)
     M = np.zeros((N, N)); df = np.zeros(N); pout = np.zeros(N); e = C.c_double()
-    rc = lib().oracle_calc_new_pop(cp.ptr, cl.ptr, layer, abi.dptr(pin), overlap, abi.dptr(M),
+    rc = lib(ref).oracle_calc_new_pop(cp.ptr, cl.ptr, layer, abi.dptr(pin), overlap, abi.dptr(M),
                                    abi.dptr(df), abi.dptr(pout), C.byref(e))
     assert rc == 0
     return M, df, pout, e.value
 
 
-def boundary_layer_populations(prob, layers):
+def boundary_layer_populations(prob, layers, ref: bool = False):
     cp, cl = prob.to_c(), layers.to_c()
     out = np.zeros((layers.nb_lay, prob.mol.nb_lev))
-    lib().oracle_boundary_layer_populations(cp.ptr, cl.ptr, abi.dptr(out))
+    lib(ref).oracle_boundary_layer_populations(cp.ptr, cl.ptr, abi.dptr(out))
     return out
 
 
