@@ -91,6 +91,9 @@ constexpr double MIN_LINE_OPACITY      = 1.e-99;
 #ifndef LVG_PANEL_ONEWAVE
 #define LVG_PANEL_ONEWAVE 2
 #endif
+#ifndef LVG_LU_MFMA
+#define LVG_LU_MFMA 0                 // 1: rank-16 updates on the matrix cores (block_lu_solve_mfma; 471K vs 511K layer-it/s, kept as a variant)
+#endif
 #ifndef LVG_OCC
 #define LVG_OCC 2                     // resident workgroups per CU solve_kernel is built for
 #endif
@@ -120,6 +123,7 @@ struct Smem {
     union alignas(16) {
         double P[NMAX][NB + 1]; // panel, physical rows
         double LT[NB][NMAX];    // L of one chunk, transposed, physical rows
+        double Ub1[NB][WB + 2]; // MFMA LU: second U buffer of the earlier-chunk steps
         double hist_acc[32];    // accel_step sums (used outside the LU only)
     } pu;
     // per-layer scalars
@@ -889,6 +893,83 @@ __device__ __forceinline__ void panel_factor_wave(double *A, int N, int kk, int 
     __syncthreads();
 }
 
+// ---- back substitution U x = y in logical order, blocked by NB from the bottom:
+//      wave 0 solves the diagonal block through LDS, then all threads update the
+//      rows above; every entry receives its updates for k descending (oracle order).
+//      b: LDS [N] by physical row; on return sm.blog holds x (logical = level order).
+__device__ __forceinline__ void back_substitute(const double *A, int N, const double *b, Smem &sm) {
+    const int t = threadIdx.x;
+    TSTAMP(tb0);
+    for (int i = t; i < N; i += BT) sm.blog[i] = b[sm.perm[i]];
+    __syncthreads();
+    const int nblk = (N + NB - 1) / NB;
+    // operands of block kb, loaded one block ahead so their latency hides behind the
+    // diagonal solve: the 16x16 diagonal block (one entry per thread) and the U
+    // segment U[perm[t]][k0..k0+nb) of this thread's row (rows above the block)
+    auto load_blk = [&](int kb, double &dv, double (&u)[NB]) {
+        const int k0 = kb * NB, nb = min(NB, N - k0);
+        const int r = t / NB, c = t - r * NB;
+        dv = (r < nb && c < nb) ? A[(int64_t)sm.perm[k0 + r] * N + k0 + c] : 0.;
+        const double *row = A + (int64_t)sm.perm[t < k0 ? t : 0] * N + k0;
+        if ((N & 1) == 0 && nb == NB) {
+            const double2 *r2 = reinterpret_cast<const double2 *>(row);
+#pragma unroll
+            for (int m = 0; m < NB / 2; m++) {
+                const double2 v = (t < k0) ? r2[m] : make_double2(0., 0.);
+                u[2 * m] = v.x;
+                u[2 * m + 1] = v.y;
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < NB; m++) u[m] = (t < k0 && m < nb) ? row[m] : 0.;
+        }
+    };
+    double dcur, ucur[NB], dnxt = 0., unxt[NB];
+    load_blk(nblk - 1, dcur, ucur);
+    for (int kb = nblk - 1; kb >= 0; kb--) {
+        const int k0 = kb * NB, nb = min(NB, N - k0);
+        {
+            const int r = t / NB, c = t - r * NB;
+            if (r < nb && c < nb) sm.L11[r][c] = dcur;
+        }
+        __syncthreads();
+        if (kb > 0) load_blk(kb - 1, dnxt, unxt);
+        if (t < 64) {
+            // diagonal block by wave 0 in registers: lane r < nb holds b_r and row r of the
+            // block; x_m (lane m's b_m / U_mm once final) is broadcast by DPP row_newbcast:m
+            const int r = t & 15;
+            double bt = (t < nb) ? sm.blog[k0 + t] : 0., ur[NB];
+#pragma unroll
+            for (int m = 0; m < NB; m++) ur[m] = (t < nb) ? sm.L11[r][m] : 1.;
+#define LVG_BSUB_STEP(M_)                                                                  \
+            if ((M_) < nb) {                                                               \
+                const double xm = dpp_d<0x150 + (M_), 0xf, 0xf>(bt / ur[M_]);              \
+                if (r < (M_)) bt = fma(-ur[M_], xm, bt);                                   \
+                else if (r == (M_)) bt = xm;                                               \
+            }
+            LVG_BSUB_STEP(15) LVG_BSUB_STEP(14) LVG_BSUB_STEP(13) LVG_BSUB_STEP(12)
+            LVG_BSUB_STEP(11) LVG_BSUB_STEP(10) LVG_BSUB_STEP(9) LVG_BSUB_STEP(8)
+            LVG_BSUB_STEP(7) LVG_BSUB_STEP(6) LVG_BSUB_STEP(5) LVG_BSUB_STEP(4)
+            LVG_BSUB_STEP(3) LVG_BSUB_STEP(2) LVG_BSUB_STEP(1) LVG_BSUB_STEP(0)
+#undef LVG_BSUB_STEP
+            if (t < nb) sm.blog[k0 + t] = bt;
+        }
+        __syncthreads();
+        if (t < k0) {
+            double s = sm.blog[t];
+#pragma unroll
+            for (int m = NB - 1; m >= 0; m--)
+                if (m < nb) s = fma(-ucur[m], sm.blog[k0 + m], s);
+            sm.blog[t] = s;
+        }
+        __syncthreads();
+        dcur = dnxt;
+#pragma unroll
+        for (int m = 0; m < NB; m++) ucur[m] = unxt[m];
+    }
+    TACC(PH_BACKSUB, tb0);
+}
+
 __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Smem &sm, const LuSrc &src, const bool FUSED) {
     const int t = threadIdx.x;
     const int rg = t >> 3, cg = t & 7;
@@ -1229,78 +1310,342 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             TACC(PH_GEMM, tp3);
         }
     }
-    TSTAMP(tb0);
-    // ---- back substitution U x = y in logical order, blocked by NB from the bottom:
-    //      wave 0 solves the diagonal block through LDS, then all threads update the
-    //      rows above; every entry receives its updates for k descending (oracle order)
-    for (int i = t; i < N; i += BT) sm.blog[i] = b[sm.perm[i]];
-    __syncthreads();
-    const int nblk = (N + NB - 1) / NB;
-    // operands of block kb, loaded one block ahead so their latency hides behind the
-    // diagonal solve: the 16x16 diagonal block (one entry per thread) and the U
-    // segment U[perm[t]][k0..k0+nb) of this thread's row (rows above the block)
-    auto load_blk = [&](int kb, double &dv, double (&u)[NB]) {
-        const int k0 = kb * NB, nb = min(NB, N - k0);
-        const int r = t / NB, c = t - r * NB;
-        dv = (r < nb && c < nb) ? A[(int64_t)sm.perm[k0 + r] * N + k0 + c] : 0.;
-        const double *row = A + (int64_t)sm.perm[t < k0 ? t : 0] * N + k0;
-        if ((N & 1) == 0 && nb == NB) {
-            const double2 *r2 = reinterpret_cast<const double2 *>(row);
-#pragma unroll
-            for (int m = 0; m < NB / 2; m++) {
-                const double2 v = (t < k0) ? r2[m] : make_double2(0., 0.);
-                u[2 * m] = v.x;
-                u[2 * m + 1] = v.y;
-            }
-        } else {
-#pragma unroll
-            for (int m = 0; m < NB; m++) u[m] = (t < k0 && m < nb) ? row[m] : 0.;
-        }
-    };
-    double dcur, ucur[NB], dnxt = 0., unxt[NB];
-    load_blk(nblk - 1, dcur, ucur);
-    for (int kb = nblk - 1; kb >= 0; kb--) {
-        const int k0 = kb * NB, nb = min(NB, N - k0);
-        {
-            const int r = t / NB, c = t - r * NB;
-            if (r < nb && c < nb) sm.L11[r][c] = dcur;
-        }
-        __syncthreads();
-        if (kb > 0) load_blk(kb - 1, dnxt, unxt);
-        if (t < 64) {
-            // diagonal block by wave 0 in registers: lane r < nb holds b_r and row r of the
-            // block; x_m (lane m's b_m / U_mm once final) is broadcast by DPP row_newbcast:m
-            const int r = t & 15;
-            double bt = (t < nb) ? sm.blog[k0 + t] : 0., ur[NB];
-#pragma unroll
-            for (int m = 0; m < NB; m++) ur[m] = (t < nb) ? sm.L11[r][m] : 1.;
-#define LVG_BSUB_STEP(M_)                                                                  \
-            if ((M_) < nb) {                                                               \
-                const double xm = dpp_d<0x150 + (M_), 0xf, 0xf>(bt / ur[M_]);              \
-                if (r < (M_)) bt = fma(-ur[M_], xm, bt);                                   \
-                else if (r == (M_)) bt = xm;                                               \
-            }
-            LVG_BSUB_STEP(15) LVG_BSUB_STEP(14) LVG_BSUB_STEP(13) LVG_BSUB_STEP(12)
-            LVG_BSUB_STEP(11) LVG_BSUB_STEP(10) LVG_BSUB_STEP(9) LVG_BSUB_STEP(8)
-            LVG_BSUB_STEP(7) LVG_BSUB_STEP(6) LVG_BSUB_STEP(5) LVG_BSUB_STEP(4)
-            LVG_BSUB_STEP(3) LVG_BSUB_STEP(2) LVG_BSUB_STEP(1) LVG_BSUB_STEP(0)
-#undef LVG_BSUB_STEP
-            if (t < nb) sm.blog[k0 + t] = bt;
-        }
-        __syncthreads();
-        if (t < k0) {
-            double s = sm.blog[t];
-#pragma unroll
-            for (int m = NB - 1; m >= 0; m--)
-                if (m < nb) s = fma(-ucur[m], sm.blog[k0 + m], s);
-            sm.blog[t] = s;
-        }
-        __syncthreads();
-        dcur = dnxt;
-#pragma unroll
-        for (int m = 0; m < NB; m++) ucur[m] = unxt[m];
+    back_substitute(A, N, b, sm);
+    double emax = 0.;
+    if (FUSED && t < N) { src.df[t] = s_acc; emax = fabs(s_acc); }
+    return FUSED ? block_max(emax, sm) : 0.;
+}
+
+
+// ------------------------------------------------------------------------------
+// Left-looking blocked LU with the rank-16 updates on the matrix cores (default).
+//
+// v_mfma_f64_16x16x4_f64 computes D = C + sum_k A[.][k] B[k][.] as a chain of fp64
+// fmas in k order (probed bit for bit: tools/probe/mfma_f64_probe.hip), so the
+// per-element update sequence fma(-l_ik, u_kj, a_ij), k ascending, of the unblocked
+// oracle LU is preserved exactly. The MFMA runs on the matrix pipe, beside the VALU
+// work (panel, TRSM, assembly) of this and the co-resident workgroup.
+//
+// Layout: the 32-column block column is held as 16x16 tiles in MFMA accumulators,
+// transposed (M = columns, N = rows), with the M index m standing for column
+// 4(m&3) + (m>>2): lane l of tile (rt, ct) holds row 16rt + (l&15) and the four
+// consecutive columns 16ct + 4(l>>4) + r, r = 0..3 (32-byte vector loads and stores).
+// Row tiles belong to waves round-robin
+// (wave w: rt = w, w+4, w+8, w+12), so each wave's rows, and the L values that
+// update them, are private to it: L goes global -> registers as MFMA B operands
+// (no LDS staging). Rows are in logical order as of the block load (tile row =
+// perm at the load), so for an earlier chunk kk the pivot rows are exactly row tile
+// kk/16 and the rows below are the tiles after it. Per earlier chunk: the owner wave
+// of tile kk/16 solves its pivot rows against L11 in registers (DPP row_newbcast:
+// the 16 rows of a column are one 16-lane DPP row), publishes U in LDS (double
+// buffered) and to A; one barrier; every wave updates its tiles below.
+// ------------------------------------------------------------------------------
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+// workgroup barrier that orders LDS only: outstanding global loads stay in flight
+// (__syncthreads()' fence would wait for them: vmcnt(0)); global stores made before it
+// are read only after a later __syncthreads().
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ v4d mfma_f64(double a, double b, v4d c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// forward substitution of one column set against L11 (lane row = l & 15): x_m -= L11[m][j] x_j,
+// j ascending (oracle order); x_j broadcast from lane j of the lane's 16-lane row.
+template <int NV>
+__device__ __forceinline__ void trsm16(double (&x)[NV], const double (&lrw)[NB], int nb, int ln) {
+#define LVG_T16_STEP(M_)                                                                   \
+    if ((M_) < nb - 1) {                                                                   \
+        _Pragma("unroll") for (int q = 0; q < NV; q++) {                                   \
+            const double y = dpp_d<0x150 + (M_), 0xf, 0xf>(x[q]);                          \
+            if (ln > (M_)) x[q] = fma(-lrw[M_], y, x[q]);                                  \
+        }                                                                                  \
     }
-    TACC(PH_BACKSUB, tb0);
+    LVG_T16_STEP(0) LVG_T16_STEP(1) LVG_T16_STEP(2) LVG_T16_STEP(3)
+    LVG_T16_STEP(4) LVG_T16_STEP(5) LVG_T16_STEP(6) LVG_T16_STEP(7)
+    LVG_T16_STEP(8) LVG_T16_STEP(9) LVG_T16_STEP(10) LVG_T16_STEP(11)
+    LVG_T16_STEP(12) LVG_T16_STEP(13) LVG_T16_STEP(14)
+#undef LVG_T16_STEP
+}
+
+__device__ __forceinline__ double block_lu_solve_mfma(double *A, int N, double *b, Smem &sm, const LuSrc &src,
+                                                      const bool FUSED) {
+    const int t = threadIdx.x, l = t & 63, ln = l & 15, lg = l >> 4;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);   // wave-uniform: scalar branches on tiles
+    const int ntl = (N + 15) >> 4;                 // row tiles
+    const int cs = 4 * (ln & 3) + (ln >> 2);       // column of MFMA M index ln within a tile
+    double s_acc = (t == 0) ? 1. : 0.;             // residual row t (FUSED)
+    for (int i = t; i < N; i += BT) { sm.perm[i] = i; sm.pos[i] = i; }
+    __syncthreads();
+    for (int c0 = 0; c0 < N; c0 += WB) {
+        TSTAMP(tp0);
+        const int wJ = min(WB, N - c0);
+        if (t < N) sm.tmap[t] = sm.perm[t];
+        __syncthreads();
+        int prow[4];                               // physical row of this lane in each own tile (-1: none)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int row = 16 * (w + 4 * i) + ln;
+            prow[i] = row < N ? sm.tmap[row] : -1;
+        }
+        // ---- block column c0..c0+wJ-1 into the accumulators (fused assembly)
+        v4d acc[4][2];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++) {
+                const int col = 16 * ct + 4 * lg, pr = prow[i], d0 = c0 + col;
+                const bool ok = pr >= 0 && col < wJ;
+                const int64_t o = (int64_t)(ok ? pr : 0) * N + d0;
+                double v[4] = {0., 0., 0., 0.};
+                int li[4] = {-1, -1, -1, -1};
+                if ((N & 3) == 0 && col + 4 <= wJ) {   // 32-byte aligned segment
+                    const double *sp = FUSED ? src.K : A;
+                    const double2 v0 = ok ? reinterpret_cast<const double2 *>(sp + o)[0] : make_double2(0., 0.);
+                    const double2 v1 = ok ? reinterpret_cast<const double2 *>(sp + o)[1] : make_double2(0., 0.);
+                    v[0] = v0.x; v[1] = v0.y; v[2] = v1.x; v[3] = v1.y;
+                    if (FUSED) {
+                        const int4 l4 = ok ? *reinterpret_cast<const int4 *>(src.li + o) : make_int4(-1, -1, -1, -1);
+                        li[0] = l4.x; li[1] = l4.y; li[2] = l4.z; li[3] = l4.w;
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const bool okr = ok && col + r < wJ;
+                        v[r] = okr ? (FUSED ? src.K[o + r] : A[o + r]) : 0.;
+                        if (FUSED) li[r] = okr ? src.li[o + r] : -1;
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    double x = v[r];
+                    const int d = d0 + r;
+                    if (FUSED && ok && col + r < wJ) {
+                        if (li[r] >= 0) x = x + src.y[li[r]];
+                        if (pr == d) x = sm.diag[d];
+                        if (pr == 0) x = 1.;
+                        if (src.dump) src.dump[o + r] = x;
+                    }
+                    acc[i][ct][r] = x;
+                }
+            }
+        if (FUSED) {
+            // residual rows: 16 columns at a time through LDS, each thread its own row
+            for (int h = 0; h < wJ; h += NB) {
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++)
+                        if (prow[i] >= 0) sm.pu.P[prow[i]][4 * lg + r] = (h == 0) ? acc[i][0][r] : acc[i][1][r];
+                __syncthreads();
+                const int nc = min(NB, wJ - h);
+                if (t < N)
+                    for (int c = 0; c < nc; c++) s_acc = s_acc - sm.pu.P[t][c] * src.pop[c0 + h + c];
+                __syncthreads();
+            }
+        }
+        TACC(PH_BLOAD, tp0);
+        for (int kk = 0; kk < c0 + wJ; kk += NB) {
+            const int nb = min(NB, N - kk);
+            if (kk < c0) {
+                // ---- earlier chunks kk = 0, 16, .., c0 - 16 (all of them in this inner loop):
+                //      pivot rows = row tile R (owner wave R & 3), rows below = tiles > R.
+                //      The next chunk's L11 (one entry per thread, to LDS) and L operands are
+                //      loaded during the current step.
+                // B operands L[row][k2 + 4g + lg] of this wave's tiles for chunk k2, loaded raw and
+                // unconditionally (no VALU op on the register and no branch around the load, so the
+                // compiler's vmcnt counting keeps them in flight until the MFMA that uses them; the
+                // sign goes on the U operand). Rows past N read row 0 and tiles above the chunk get
+                // values that are never used: neither is ever stored.
+                int prc[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) prc[i] = prow[i] >= 0 ? prow[i] : 0;
+                auto load_lf = [&](int k2, double (&lf)[4][4]) {
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const double *src_l = A + (int64_t)prc[i] * N + k2 + lg;
+#pragma unroll
+                        for (int g = 0; g < 4; g++) lf[i][g] = src_l[4 * g];
+                    }
+                };
+                // L11 rows of the next chunk this wave owns (row ln of chunk kr, final): loaded
+                // right after the wave's previous TRSM, four steps before they are used
+                auto load_l11 = [&](int kr, double (&lr)[NB]) {
+                    const double *sp = A + (int64_t)sm.tmap[kr + ln] * N + kr;
+                    if ((N & 1) == 0) {
+#pragma unroll
+                        for (int j = 0; j < NB / 2; j++) {
+                            const double2 v = reinterpret_cast<const double2 *>(sp)[j];
+                            lr[2 * j] = v.x; lr[2 * j + 1] = v.y;
+                        }
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < NB; j++) lr[j] = sp[j];
+                    }
+                };
+                const int klast = c0 - NB;
+                double lf[4][4], lrn[NB];
+                if (NB * w < c0) load_l11(NB * w, lrn);
+                load_lf(0, lf);
+                // TRSM of chunk k3 by its owner on its pivot tile (held in acc[i3]) -> Ub buffer, A
+                auto owner_trsm = [&](int k3, double (*Uo)[WB + 2]) {
+                    const int i3 = (k3 >> 4) >> 2;
+                    double x[8];
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        if (i == i3) {
+#pragma unroll
+                            for (int r = 0; r < 4; r++) { x[r] = acc[i][0][r]; x[4 + r] = acc[i][1][r]; }
+                        }
+                    TSTAMP(tp2s);
+                    trsm16<8>(x, lrn, NB, ln);
+                    const int64_t urow = (int64_t)sm.tmap[k3 + ln] * N + c0;
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        const int col = 16 * (q >> 2) + 4 * lg + (q & 3);
+                        if (col < wJ) { Uo[ln][col] = x[q]; A[urow + col] = x[q]; }
+                    }
+                    if (k3 + 4 * NB < c0) load_l11(k3 + 4 * NB, lrn);   // this wave's next chunk
+                    TACC(PH_T_SOLVE, tp2s);
+                };
+                if (w == 0) owner_trsm(0, sm.Ub);  // chunk 0: its pivot rows need no update
+                lds_barrier();
+                // Step kk applies U(kk) to the tiles below row tile R. The owner of chunk kk + 16
+                // first updates only its pivot tile, solves it (U(kk+16) into the other buffer)
+                // and issues its remaining MFMAs after the barrier; the other waves issue all of
+                // theirs before it. So the pivot chain per step is 8 MFMAs + one TRSM.
+                for (; kk < c0; kk += NB) {
+                    TSTAMP(tp3);
+                    const int R = kk >> 4, R2 = R + 1;
+                    double (*U)[WB + 2] = (R & 1) ? sm.pu.Ub1 : sm.Ub;
+                    double (*Un)[WB + 2] = (R & 1) ? sm.Ub : sm.pu.Ub1;
+                    const int k2 = min(kk + NB, klast);
+                    double u0[4], u1[4];
+#pragma unroll
+                    for (int g = 0; g < 4; g++) { u0[g] = -U[4 * g + lg][cs]; u1[g] = -U[4 * g + lg][16 + cs]; }
+                    const bool nown = kk + NB < c0 && w == (R2 & 3);
+                    const int iP = nown ? (R2 >> 2) : -1;
+                    auto upd_tile = [&](int i) {
+#pragma unroll
+                        for (int g = 0; g < 4; g++) {
+                            acc[i][0] = mfma_f64(u0[g], lf[i][g], acc[i][0]);
+                            if (wJ > 16) acc[i][1] = mfma_f64(u1[g], lf[i][g], acc[i][1]);
+                        }
+                    };
+                    auto upd_rest = [&]() {
+#pragma unroll
+                        for (int g = 0; g < 4; g++) {
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                if ((w + 4 * i) > R && (w + 4 * i) < ntl && i != iP) {
+                                    acc[i][0] = mfma_f64(u0[g], lf[i][g], acc[i][0]);
+                                    if (wJ > 16) acc[i][1] = mfma_f64(u1[g], lf[i][g], acc[i][1]);
+                                }
+                                lf[i][g] = A[(int64_t)prc[i] * N + k2 + 4 * g + lg];
+                            }
+                        }
+                    };
+                    if (nown) {
+#pragma unroll
+                        for (int i = 0; i < 4; i++)
+                            if (i == iP) upd_tile(i);
+                        owner_trsm(kk + NB, Un);
+                    }
+                    upd_rest();
+                    lds_barrier();                 // LDS only: the next chunk's L loads stay in flight
+                    TACC(PH_GEMM, tp3);
+                }
+                kk -= NB;                          // the outer loop steps to c0
+            } else {
+                // ---- a chunk of this block column: all updates from k < kk are in; factor it
+                TSTAMP(tp1);
+                const int ch = (kk - c0) >> 4;
+                if (ch == 0 && c0 > 0) __syncthreads();   // the last earlier step's U (pu.Ub1) vs P
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++)
+                        if (prow[i] >= 0) sm.pu.P[prow[i]][4 * lg + r] = ch ? acc[i][1][r] : acc[i][0][r];
+                __syncthreads();
+                const int trow = (t < N) ? sm.tmap[t] : 0;
+                if (LVG_PANEL_ONEWAVE >= 2 && (c0 >> 6) != ((N - 1) >> 6) && (c0 >> 7) == ((N - 1) >> 7)) {
+                    const int base = (c0 >> 7) << 7, lw = t & 63;
+                    const int r2[2] = {base + lw < N ? sm.tmap[base + lw] : -1, base + 64 + lw < N ? sm.tmap[base + 64 + lw] : -1};
+                    panel_factor_wave<2>(A, N, kk, nb, b, sm, base >> 6, r2);
+                } else if (LVG_PANEL_ONEWAVE && (c0 >> 6) == ((N - 1) >> 6)) {
+                    const int r1[1] = {t < N ? trow : -1};
+                    panel_factor_wave<1>(A, N, kk, nb, b, sm, c0 >> 6, r1);
+                } else {
+                    panel_factor(A, N, kk, nb, b, sm);
+                }
+                for (int e = t; e < NB * NB; e += BT) {
+                    const int r = e / NB, m = e - r * NB;
+                    sm.L11[r][m] = (r < nb && m < r) ? sm.pu.P[sm.perm[kk + r]][m] : 0.;
+                }
+                __syncthreads();
+                TACC(PH_PANEL, tp1);
+                if (kk - c0 + nb >= wJ) break;     // last chunk of the block column
+                TSTAMP(tq);
+                // pivot rows of this chunk (logical kk.., scattered over the tiles) in columns 16..31
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    if (prow[i] >= 0) {
+                        const int q = sm.pos[prow[i]] - kk;
+                        if (q >= 0 && q < nb) {
+#pragma unroll
+                            for (int r = 0; r < 4; r++) {
+                                const int col = 16 + 4 * lg + r;
+                                if (col < wJ) sm.Ub[q][col] = acc[i][1][r];
+                            }
+                        }
+                    }
+                }
+                __syncthreads();
+                if (w == 0) {
+                    double x[4], lrw[NB];
+#pragma unroll
+                    for (int r = 0; r < 4; r++) x[r] = (ln < nb && 16 + 4 * lg + r < wJ) ? sm.Ub[ln][16 + 4 * lg + r] : 0.;
+#pragma unroll
+                    for (int j = 0; j < NB; j++) lrw[j] = sm.L11[ln][j];
+                    trsm16<4>(x, lrw, nb, ln);
+                    if (ln < nb) {
+                        const int64_t urow = (int64_t)sm.perm[kk + ln] * N + c0;
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            const int col = 16 + 4 * lg + r;
+                            if (col < wJ) { sm.Ub[ln][col] = x[r]; A[urow + col] = x[r]; }
+                        }
+                    }
+                }
+                __syncthreads();
+                TACC(PH_TRSM, tq);
+                TSTAMP(tu);
+                // rows below the chunk: columns 16..31 -= L (from the panel, in P) U
+                double lf[4][4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const bool act = prow[i] >= 0 && sm.pos[prow[i]] >= kk + nb;
+#pragma unroll
+                    for (int g = 0; g < 4; g++) lf[i][g] = act ? -sm.pu.P[prow[i]][4 * g + lg] : 0.;
+                }
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const double u1 = sm.Ub[4 * g + lg][16 + cs];
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        if ((w + 4 * i) < ntl) acc[i][1] = mfma_f64(u1, lf[i][g], acc[i][1]);
+                }
+                __syncthreads();                   // P is rewritten by the next chunk
+                TACC(PH_GEMM, tu);
+            }
+        }
+    }
+    back_substitute(A, N, b, sm);
     double emax = 0.;
     if (FUSED && t < N) { src.df[t] = s_acc; emax = fabs(s_acc); }
     return FUSED ? block_max(emax, sm) : 0.;
@@ -1529,7 +1874,8 @@ __device__ __forceinline__ void solve_layer(const LvgDevProblem &P, const LvgLau
         }
         for (int i = t; i < N; i += BT) sm.bvec[i] = (i == 0) ? 1. : 0.;
         __syncthreads();
-        const double eq = block_lu_solve(S.A, N, sm.bvec, sm, src, !boundary);
+        const double eq = LVG_LU_MFMA ? block_lu_solve_mfma(S.A, N, sm.bvec, sm, src, !boundary)
+                                       : block_lu_solve(S.A, N, sm.bvec, sm, src, !boundary);
         if (boundary) {
             TACC(PH_BOUNDARY, tb0);
             for (int i = t; i < N; i += BT) { sm.pold[i] = sm.blog[i]; S.given[i] = sm.blog[i]; }
@@ -1617,7 +1963,8 @@ __global__ void __launch_bounds__(BT, 2) debug_kernel(const LvgDevProblem *__res
     __syncthreads();
     LuSrc src;
     src.K = S.K; src.y = yp; src.li = M.line_idx; src.pop = sm.pold; src.df = S.df; src.dump = Lc.dbg_matrix;
-    const double eq = block_lu_solve(S.A, N, sm.bvec, sm, src, true);
+    const double eq = LVG_LU_MFMA ? block_lu_solve_mfma(S.A, N, sm.bvec, sm, src, true)
+                                   : block_lu_solve(S.A, N, sm.bvec, sm, src, true);
     for (int i = t; i < N; i += BT) { Lc.pops[i] = sm.blog[i]; Lc.dbg_df[i] = S.df[i]; }
     if (t == 0) Lc.dbg_df[N] = eq;
 }

@@ -1,7 +1,7 @@
 """Diagnostic: per-phase cycle breakdown of the solve kernel (timer build)."""
 import ctypes as C, os, sys, time, numpy as np
 sys.path.insert(0, "/root/repo")
-os.environ["LVG_LIB_PATH"] = "/root/repo/radiative_transfer_amd/_lib/liblvg_amd_timers.so"
+os.environ.setdefault("LVG_LIB_PATH", "/root/repo/radiative_transfer_amd/_lib/liblvg_amd_timers.so")
 from radiative_transfer_amd import synth, abi, native
 names = ["setup+coll", "boundary LU", "line terms", "assemble+resid", "LU panel", "LU swap+trsm", "LU gemm", "LU backsub", "ctl",
          " (layer_setup)", " (pair tiles)", " (B diagonal)", "LU block load",
