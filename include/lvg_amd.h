@@ -27,7 +27,11 @@
  * exits. Non-convergence of a layer is NOT an error: it is reported per layer
  * in lvg_layer_status (the reference's `bad_layers`, radiative_transfer.cpp:278-288).
  *
- * Threading: one handle per host thread; calls on a handle are synchronous.
+ * Threading: one handle per host thread. Every call on a handle is synchronous
+ * except lvg_solve_layers_device with a non-NULL stream, which returns once its
+ * kernel is queued; later calls on the same handle are ordered after it (same
+ * stream: stream order; any other stream, including the handle's own: the call
+ * first waits for it), and the handle frees nothing that kernel uses before it ends.
  */
 #ifndef LVG_AMD_H
 #define LVG_AMD_H
@@ -220,7 +224,8 @@ int         lvg_solve_layers(lvg_handle *h, const lvg_layers *layers, double *po
  * in the field order of lvg_layers (temp_n, temp_el, el_conc, h_conc, ph2_conc,
  * oh2_conc, he_conc, mol_conc, vel_turb, vel_grad, then dust_conc[c]) — see
  * lvg_layer_soa_rows(). d_status: [nb_lay] lvg_layer_status. Asynchronous on
- * `stream`; LVG_INIT_WARM_CHAIN is not accepted here. */
+ * a non-NULL `stream` (see Threading above); synchronous with NULL.
+ * LVG_INIT_WARM_CHAIN is not accepted here (see lvg_solve_chains). */
 int         lvg_layer_soa_rows(const lvg_handle *h);
 int         lvg_solve_layers_device(lvg_handle *h, int nb_lay, const double *d_layer_soa,
                                     double *d_pops_inout, const lvg_solve_opts *opts,

@@ -81,6 +81,12 @@ struct lvg_handle {
     size_t sched_cap = 0, sched_tmp_cap = 0;
     double last_ms = 0.;
     int last_launches = 0;
+    // an asynchronous lvg_solve_layers_device (caller's stream) may still be running:
+    // its kernel reads the launch block, the queue counter and the workspace slots, so
+    // any later call on this handle is ordered after it (settle) and nothing it uses is
+    // freed before it ends (drain). ev1 marks its end.
+    int pending = 0;
+    hipStream_t pending_stream = nullptr;
     // device-resident parameter blocks (kernels take pointers: no kernarg copies)
     LvgDevProblem *d_prob = nullptr;
     LvgLaunch *d_launch = nullptr;
@@ -532,6 +538,20 @@ int build(lvg_handle *h, const lvg_problem *p) {
     return LVG_OK;
 }
 
+// block the host until the last asynchronous solve on this handle has finished
+void drain(lvg_handle *h) {
+    if (h->pending) {
+        (void)hipEventSynchronize(h->ev1);
+        h->pending = 0;
+    }
+}
+
+// order a call that works on stream s after the last asynchronous solve: same stream ->
+// stream order suffices; another stream -> wait for it
+void settle(lvg_handle *h, hipStream_t s) {
+    if (h->pending && s != h->pending_stream) drain(h);
+}
+
 int ensure_workspace(lvg_handle *h, int slots) {
     const int N = h->N;
     const int lines = std::max(h->P.plain.nb_lines, h->P.overlap.nb_lines);
@@ -539,6 +559,7 @@ int ensure_workspace(lvg_handle *h, int slots) {
     stride = (stride + 31) & ~31LL;
     size_t bytes = (size_t)stride * slots * sizeof(double);
     if (bytes > h->ws_bytes) {
+        drain(h);
         if (h->ws) (void)hipFree(h->ws);
         h->ws = nullptr;
         h->ws_bytes = 0;
@@ -582,6 +603,7 @@ int push_launch(lvg_handle *h, const LvgLaunch &L, int slot, hipStream_t s, cons
     if (slot >= h->n_launch_slots) {
         int n = std::max(slot + 1, 2 * h->n_launch_slots);
         LvgLaunch *p = nullptr;
+        drain(h);
         if (h->d_launch) { (void)hipStreamSynchronize(s); (void)hipFree(h->d_launch); }
         if (hipMalloc(&p, sizeof(LvgLaunch) * n) != hipSuccess) return fail(h, LVG_E_NOMEM, "launch block alloc failed");
         h->d_launch = p;
@@ -594,6 +616,7 @@ int push_launch(lvg_handle *h, const LvgLaunch &L, int slot, hipStream_t s, cons
 
 int grow(lvg_handle *h, void **p, size_t *cap, size_t bytes) {
     if (bytes <= *cap) return LVG_OK;
+    drain(h);
     if (*p) (void)hipFree(*p);
     *p = nullptr;
     *cap = 0;
@@ -631,6 +654,7 @@ int lvg_layer_soa_rows(const lvg_handle *h) { return h ? 10 + h->nb_comp : 0; }
 void lvg_destroy(lvg_handle *h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
+    drain(h);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (auto &b : h->bufs) (void)hipFree(b.p);
     if (h->ws) (void)hipFree(h->ws);
@@ -704,6 +728,7 @@ int lvg_solve_layers_device(lvg_handle *h, int nb_lay, const double *d_soa, doub
     if (nb_lay == 0) return LVG_OK;
     HIPCHECK(h, hipSetDevice(h->device));
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    settle(h, s);
     int per_cu = h->blocks_per_cu;
     if (const char *e = std::getenv("LVG_BLOCKS_PER_CU")) {   // tuning/diagnostics only
         const int v = std::atoi(e);
@@ -763,6 +788,10 @@ int lvg_solve_layers_device(lvg_handle *h, int nb_lay, const double *d_soa, doub
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, h->ev0, h->ev1);
         h->last_ms = ms;
+        h->pending = 0;
+    } else {
+        h->pending = 1;
+        h->pending_stream = s;
     }
     return LVG_OK;
 }
@@ -808,6 +837,7 @@ int lvg_solve_layers(lvg_handle *h, const lvg_layers *layers, double *pops, cons
     const int nl = layers->nb_lay, N = h->N;
     if (nl == 0) return LVG_OK;
     HIPCHECK(h, hipSetDevice(h->device));
+    settle(h, h->stream);
     if ((rc = upload_layers(h, layers))) return rc;
     if ((rc = grow(h, (void **)&h->d_pops, &h->pops_cap, sizeof(double) * (size_t)nl * N))) return rc;
     if ((rc = grow(h, &h->d_status, &h->status_cap, sizeof(lvg_layer_status) * (size_t)nl))) return rc;
@@ -865,6 +895,7 @@ int lvg_debug_calc_new_pop(lvg_handle *h, const lvg_layers *layers, int layer, c
     if (line_overlap && !h->has_overlap) return fail(h, LVG_E_ARG, "no overlap tables");
     const int N = h->N;
     HIPCHECK(h, hipSetDevice(h->device));
+    settle(h, h->stream);
     int rc = upload_layers(h, layers);
     if (rc) return rc;
     if ((rc = ensure_workspace(h, 1))) return rc;
@@ -906,6 +937,7 @@ int lvg_boundary_layer_populations(lvg_handle *h, const lvg_layers *layers, doub
     const int nl = layers->nb_lay, N = h->N;
     if (nl == 0) return LVG_OK;
     HIPCHECK(h, hipSetDevice(h->device));
+    settle(h, h->stream);
     int rc = upload_layers(h, layers);
     if (rc) return rc;
     if ((rc = grow(h, (void **)&h->d_pops, &h->pops_cap, sizeof(double) * (size_t)nl * N))) return rc;
@@ -967,6 +999,7 @@ int lvg_find_transitions(lvg_handle *h, const lvg_layers *layers, const lvg_clou
     if (nl == 0 || nlines == 0) return LVG_OK;
     if (!pops || !geo->dz || !geo->vel_n) return fail(h, LVG_E_ARG, "lvg_find_transitions: pops / dz / vel_n missing");
     HIPCHECK(h, hipSetDevice(h->device));
+    settle(h, h->stream);
     int rc = upload_layers(h, layers);
     if (rc) return rc;
     TmpDev T;
@@ -1060,6 +1093,7 @@ int lvg_lim_luminosity(lvg_handle *h, const lvg_layers *layers, const lvg_cloud_
         if (up[t] <= low[t] || low[t] < 0 || up[t] >= N) return fail(h, LVG_E_ARG, "transition %d: need N > up > low >= 0", t);
     if (2 * nb_trans > N * N) return fail(h, LVG_E_UNSUPPORTED, "too many transitions for the slot scratch");
     HIPCHECK(h, hipSetDevice(h->device));
+    settle(h, h->stream);
     int rc = upload_layers(h, layers);
     if (rc) return rc;
     if ((rc = grow(h, (void **)&h->d_pops, &h->pops_cap, sizeof(double) * (size_t)nl * N))) return rc;

@@ -700,7 +700,11 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
             // |v| >= 0 orders like its bit pattern; active rows carry the top bit
             const double av = fabs(rw[c]);
             const unsigned long long bits = (act && av == av) ? (unsigned long long)__double_as_longlong(av) : 0ull;
-            const unsigned hi = act ? ((unsigned)(bits >> 32) | 0x80000000u) : 0u, lo = (unsigned)bits;
+            // oracle_lu_solve seeds amax with |a_kk| and replaces it on a strict '>': a NaN
+            // below never wins, a NaN on the diagonal (logical position c) always does
+            const bool dnan = act && lp == c && av != av;
+            const unsigned hi = dnan ? 0xffffffffu : act ? ((unsigned)(bits >> 32) | 0x80000000u) : 0u;
+            const unsigned lo = dnan ? 0xffffffffu : (unsigned)bits;
             TSTAMP(tpr);
             const unsigned H = wave_max_u32(hi);
             unsigned Lw;
@@ -824,7 +828,9 @@ __device__ __forceinline__ void panel_factor_wave(double *A, int N, int kk, int 
                     const double av = fabs(rw[i][c]);
                     const unsigned long long bits =
                         (act[i] && av == av) ? (unsigned long long)__double_as_longlong(av) : 0ull;
-                    const unsigned hi = act[i] ? ((unsigned)(bits >> 32) | 0x80000000u) : 0u, lo = (unsigned)bits;
+                    const bool dnan = act[i] && lp[i] == c && av != av;   // NaN diagonal wins (oracle rule)
+                    const unsigned hi = dnan ? 0xffffffffu : act[i] ? ((unsigned)(bits >> 32) | 0x80000000u) : 0u;
+                    const unsigned lo = dnan ? 0xffffffffu : (unsigned)bits;
                     const bool better = hi > bh || (hi == bh && (lo > bl || (lo == bl && (unsigned)lp[i] < (unsigned)bp)));
                     bh = better ? hi : bh;
                     bl = better ? lo : bl;

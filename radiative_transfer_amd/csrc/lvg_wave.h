@@ -332,7 +332,11 @@ __device__ __forceinline__ void wave_lu_solve(double (&a)[NM], double rb, int N,
         if (c < N) {
             const double av = fabs(a[c]);
             const unsigned long long bits = (act && av == av) ? (unsigned long long)__double_as_longlong(av) : 0ull;
-            const unsigned hi = act ? ((unsigned)(bits >> 32) | 0x80000000u) : 0u, lo = (unsigned)bits;
+            // oracle_lu_solve: amax seeded with |a_kk|, replaced on a strict '>' -> a NaN below
+            // never wins, a NaN on the diagonal (logical position c) always does
+            const bool dnan = act && lp == c && av != av;
+            const unsigned hi = dnan ? 0xffffffffu : act ? ((unsigned)(bits >> 32) | 0x80000000u) : 0u;
+            const unsigned lo = dnan ? 0xffffffffu : (unsigned)bits;
             const unsigned H = wave_max_u32(hi);
             const unsigned long long tie = __ballot(hi == H);
             int pl;

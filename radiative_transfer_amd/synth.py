@@ -173,6 +173,9 @@ def oh_hf(rng, N=24):
     Jvals = [1.5, 1.5, 2.5, 2.5, 0.5, 0.5, 3.5, 3.5, 1.5, 1.5, 4.5, 4.5, 2.5, 2.5, 5.5, 5.5]
     base = [0.0, 0.0556, 83.72, 83.84, 126.29, 126.45, 187.49, 187.70, 188.45, 188.79,
             289.16, 289.48, 288.60, 289.0, 415.5, 416.0]
+    for p in range(16, npar):          # more Lambda doublets for larger N (the reference's OH-HF has 56 levels)
+        Jvals.append(Jvals[p - 8] + 2.0)
+        base.append(base[p - 2] + 130.0 + (0.3 if p % 2 else 0.0))
     par_e = np.sort(np.array(base[:npar]) + rng.uniform(0, 0.02, npar) * (np.arange(npar) % 2))
     par_e = np.maximum.accumulate(par_e + np.arange(npar) * 1e-3)
     Jp = np.array(Jvals[:npar])

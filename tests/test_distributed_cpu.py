@@ -30,9 +30,14 @@ def _worker(rank, world, port, name, nl, out):
     opts = abi.default_opts(**o)
     pops, st, totals = dist.solve_sharded(L, lambda sub: oracle.solve_layers(P, sub, opts, nthreads=1),
                                           P.mol.nb_lev, gather=True)
+    # bench.py's per-step reduction of a device-layout status tensor (here on the CPU)
+    import torch
+    lo, hi = dist.shard_range(nl, world, rank)
+    raw = np.frombuffer(st[lo:hi].tobytes(), dtype=np.float64).reshape(hi - lo, abi.STATUS_DTYPE.itemsize // 8)
+    dev_tot = dist.reduce_status_device(torch.from_numpy(raw.copy())).numpy()
     if rank == 0:
         np.savez(out, pops=pops, iters=st["iterations"], conv=st["converged"],
-                 totals=np.array([totals[0], totals[1]]), relmax=np.array([totals[2]]))
+                 totals=np.array([totals[0], totals[1]]), relmax=np.array([totals[2]]), dev_tot=dev_tot)
     td.barrier()
     td.destroy_process_group()
 
@@ -46,7 +51,8 @@ def test_shard_range_partitions():
             assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
 
 
-@pytest.mark.parametrize("name,nl", [("ph2o45_1024", 10), ("oh24_overlap_2048", 6)])
+# nl=1 < world: rank 1's block is empty (it must neither crash nor hang the all_gather)
+@pytest.mark.parametrize("name,nl", [("ph2o45_1024", 10), ("oh24_overlap_2048", 6), ("ph2o45_1024", 1)])
 def test_gloo_world2_matches_single_process(tmp_path, name, nl):
     from oracle import oracle
     out = str(tmp_path / "r0.npz")
@@ -59,3 +65,4 @@ def test_gloo_world2_matches_single_process(tmp_path, name, nl):
     assert got["totals"][0] == st["iterations"].sum()
     assert got["totals"][1] == (st["converged"] == 0).sum()
     assert got["relmax"][0] == st["rel_error"].max()
+    assert np.array_equal(got["dev_tot"], [st["iterations"].sum(), (st["converged"] == 0).sum(), st["rel_error"].max()])

@@ -10,6 +10,7 @@ import pytest
 from radiative_transfer_amd import abi, synth
 from radiative_transfer_amd.native import LvgError, LvgSolver
 from oracle import oracle
+from parity_helpers import assert_same
 
 pytestmark = pytest.mark.gpu
 
@@ -22,16 +23,6 @@ def solver_for(name, nb_lay=None, nb_lev=None):
     if key not in _solvers:
         _solvers[key] = LvgSolver(P)
     return _solvers[key], P, L, o
-
-
-def assert_same(pg, sg, po, so):
-    assert np.array_equal(sg["iterations"], so["iterations"]), (sg["iterations"], so["iterations"])
-    assert np.array_equal(sg["converged"], so["converged"])
-    assert np.array_equal(sg["used_plain_retry"], so["used_plain_retry"])
-    for f in ("eq_error", "rel_error", "pop_error"):
-        assert np.array_equal(sg[f], so[f]), f
-    bad = np.argwhere(pg != po)
-    assert bad.size == 0, f"{len(bad)} population entries differ, first {bad[:3].tolist()}"
 
 
 CASES = [("oh24_single", 1, None), ("ph2o45_1024", 48, None), ("oh24_overlap_2048", 24, None),

@@ -20,14 +20,14 @@ import numpy as np
 import pytest
 
 import ingest_files as W
+import ingest_problem as IP
 from oracle import ingest as O
+from ingest_problem import (CH3OH_NL, ANG_MAX, FILE_LEV, FILE_LEV_ROVIBR, FILE_LEV_OH2, H2O_NL, OH_NL,
+                            JOIN_NB)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "tests", "cpp", "_build", "test_ingest")
 
-CH3OH_NL, ANG_MAX = 60, 8
-FILE_LEV, FILE_LEV_ROVIBR, FILE_LEV_OH2 = 40, 30, 25
-H2O_NL, OH_NL, JOIN_NB = 45, 20, 3
 
 
 def _build():
@@ -36,65 +36,12 @@ def _build():
     subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")])
 
 
-def _load(out):
-    arrs = {}
-    with open(os.path.join(out, "manifest.txt")) as f:
-        for line in f:
-            name, dt, n = line.split()
-            a = np.fromfile(os.path.join(out, name + ".bin"), dtype=np.float64 if dt == "f8" else np.int32)
-            assert a.size == int(n), name
-            arrs[name] = a
-    return arrs
-
-
 @pytest.fixture(scope="module")
 def ingest(tmp_path_factory):
     _build()
     d = str(tmp_path_factory.mktemp("data")) + "/"
     out = str(tmp_path_factory.mktemp("out")) + "/"
-    rng = np.random.default_rng(2024)
-    truth = {}
-    # CH3OH-A
-    blocks = W.ch3oh_levels_truth(rng)
-    W.write_ch3oh_levels(d, blocks)
-    ch = O.ch3oh_diagram(blocks, 1.5, CH3OH_NL, 2, ANG_MAX)
-    alev = W.a_levels(blocks, nb_vibr=2, ang_mom_max=10)        # a pool wider than the diagram
-    pool = [(v, J, K) for v, J, K, _ in alev]
-    inside = [(l["v"], int(l["j"]), int(l["k1"])) for l in ch.lev]
-    lines = []
-    for q in range(300):
-        src = inside if q % 4 else pool          # mostly levels of the diagram, some absent
-        a, b = rng.choice(len(src), 2, replace=False)
-        lines.append(src[a] + src[b] + (float(rng.uniform(0.1, 5.0)),))
-    W.write_ch3oh_radiative(d, lines)
-    truth["ch3oh_coll"] = W.write_ch3oh_coll(d, rng, pool, FILE_LEV, FILE_LEV_ROVIBR, FILE_LEV_OH2)
-    # p-H2O
-    rows = W.h2o_levels_truth(rng)
-    W.write_h2o_levels(d, rows)
-    hw = O.h2o_diagram(rows, 0., H2O_NL)
-    hlines = []
-    for _ in range(200):
-        a, b = rng.choice(len(rows), 2, replace=False)
-        hlines.append((rows[a][:6], rows[b][:6], float(rng.uniform(1e-6, 1e-2))))
-    W.write_h2o_radiative(d, hlines)
-    truth["h2o_coll"] = W.write_h2o_coll(d, rng, [O.h2o_label(hw, i) for i in range(hw.n)])
-    # OH hyperfine
-    orows = W.oh_levels_truth(rng, 24)
-    W.write_oh_levels(d, orows)
-    oh = O.oh_diagram(orows, OH_NL)
-    olines = []
-    for _ in range(60):
-        a, b = rng.choice(len(orows), 2, replace=False)
-        olines.append((orows[a][:5], orows[b][:5], float(rng.uniform(1e-11, 1e-9))))
-    W.write_oh_radiative(d, olines)
-    truth["oh_coll"] = W.write_oh_coll(d, rng, 24)
-    # cloud
-    truth["cloud"] = W.write_cloud(d, rng)
-    r = subprocess.run([EXE, d, out, str(CH3OH_NL), str(ANG_MAX), str(FILE_LEV), str(FILE_LEV_ROVIBR),
-                        str(FILE_LEV_OH2), str(H2O_NL), str(OH_NL), str(JOIN_NB)],
-                       capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0 and "INGEST OK" in r.stdout, (r.stdout, r.stderr)
-    return dict(got=_load(out), truth=truth, ch=ch, ch_lines=lines, hw=hw, h_lines=hlines, oh=oh, o_lines=olines)
+    return IP.write_and_ingest(d, out, EXE)
 
 
 def _check_diagram(got, prefix, di):
