@@ -6,7 +6,10 @@ layer-sharded over the ranks with dist.shard_range — strong scaling: `--gpus N
 the same 4096 layers N ways (`--weak` keeps 4096 layers per GPU instead).
 `--workload` selects the other BASELINE configs for their own lines: ph2o45_1024
 (configs[1]), ch3ohe256_sweep (configs[3], 128x128 = 16384 cells), oh24_overlap_2048
-(configs[4]).
+(configs[4]). `--chain-len C` switches to the reference's default start rule
+(LVG_INIT_WARM_CHAIN, radiative_transfer.cpp:247-252): the rank's layers become
+independent clouds of C consecutive layers, each a warm chain, all solved in one
+launch (lvg_solve_chains_device; one workgroup / wave per chain).
 
 A "step" is one full batched solve of this rank's layers: per layer the collision
 operator, boundary_layer_populations, and the iteration_control loop (calc_new_pop =
@@ -92,30 +95,42 @@ def host_info() -> dict:
     return info
 
 
-def cpu_leg(prob, layers, opts, budget_s: float, threads: int):
-    """Oracle (C restatement, OpenMP schedule(dynamic,1) over layers) on a bounded sample."""
+def cpu_leg(prob, layers, opts, budget_s: float, threads: int, chain_len: int = 0):
+    """Oracle (C restatement, OpenMP schedule(dynamic,1) over layers, or over clouds for
+    warm chains as the reference's shock-model loop) on a bounded sample."""
     from oracle import oracle
     oracle.build()
     done = its = 0
     chunk = max(8, 4 * threads)
+    if chain_len:
+        chunk = chain_len * max(1, threads)
     t0 = time.perf_counter()
     while done < layers.nb_lay and time.perf_counter() - t0 < budget_s:
         idx = np.arange(done, min(done + chunk, layers.nb_lay))
-        _, st = oracle.solve_layers(prob, layers.subset(idx), opts, nthreads=threads)
+        sub = layers.subset(idx)
+        if chain_len:
+            _, st = oracle.solve_chains(prob, sub, chain_offsets(idx.size, chain_len), opts, nthreads=threads)
+        else:
+            _, st = oracle.solve_layers(prob, sub, opts, nthreads=threads)
         its += int(st["iterations"].sum())
         done += idx.size
     dt = time.perf_counter() - t0
     return its / dt, f"first {done} of {layers.nb_lay} layers ({its} layer-iterations, {dt:.1f} s)"
 
 
-def cpu_baseline(prob, layers, opts, budget_s: float):
+def chain_offsets(n: int, chain_len: int) -> np.ndarray:
+    """Clouds of chain_len consecutive layers (the last one shorter)."""
+    return np.unique(np.r_[np.arange(0, n, chain_len), n]).astype(np.int32)
+
+
+def cpu_baseline(prob, layers, opts, budget_s: float, chain_len: int = 0):
     info = host_info()
     # all the CPUs this process may use; the GPU box caps a job's share (OMP_NUM_THREADS)
     threads = info["affinity_cpus"]
     if info["omp_num_threads"] and info["omp_num_threads"].isdigit():
         threads = min(threads, int(info["omp_num_threads"]))
-    v_all, s_all = cpu_leg(prob, layers, opts, budget_s, threads)
-    v_one, s_one = cpu_leg(prob, layers, opts, budget_s, 1)
+    v_all, s_all = cpu_leg(prob, layers, opts, budget_s, threads, chain_len)
+    v_one, s_one = cpu_leg(prob, layers, opts, budget_s, 1, chain_len)
     return {"value": v_all, "unit": UNIT, "cores": threads, "kind": "port",
             "sample": f"{s_all}, oracle/lvg_oracle.c -O3 OpenMP schedule(dynamic,1), {threads} threads",
             "one_thread": {"value": v_one, "unit": UNIT, "cores": 1, "sample": s_one},
@@ -130,6 +145,8 @@ def main():
     ap.add_argument("--workload", default="ch3oha256_4096")
     ap.add_argument("--layers", type=int, default=0, help="cloud layers (default: the config's)")
     ap.add_argument("--weak", action="store_true", help="config's layers PER GPU instead of one cloud")
+    ap.add_argument("--chain-len", type=int, default=0,
+                    help="warm chains of this many layers (LVG_INIT_WARM_CHAIN) instead of independent layers")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds per CPU leg")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-entry", action="store_true")
@@ -156,6 +173,8 @@ def main():
     total = L_cloud * world if args.weak else L_cloud
     prob, layers_all, o = synth.make_problem(args.workload, nb_lay=total)
     opts = abi.default_opts(**o)
+    if args.chain_len:
+        opts.init = abi.LVG_INIT_WARM_CHAIN
     lo, hi = dist.shard_range(total, world, rank)
     mine = layers_all.subset(np.arange(lo, hi))
     n_mine = hi - lo
@@ -166,9 +185,15 @@ def main():
     status = torch.zeros((max(n_mine, 1), abi.STATUS_DTYPE.itemsize // 8), dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev)
 
+    offs = chain_offsets(n_mine, args.chain_len) if args.chain_len else None
+
     def step():
-        solver.solve_layers_device(n_mine, soa.data_ptr(), pops.data_ptr(), status.data_ptr(), opts,
-                                   stream_ptr=stream.cuda_stream)
+        if offs is not None:
+            solver.solve_chains_device(n_mine, soa.data_ptr(), offs, pops.data_ptr(), status.data_ptr(), opts,
+                                       stream_ptr=stream.cuda_stream)
+        else:
+            solver.solve_layers_device(n_mine, soa.data_ptr(), pops.data_ptr(), status.data_ptr(), opts,
+                                       stream_ptr=stream.cuda_stream)
         return dist.reduce_status_device(status[:n_mine])
 
     for _ in range(max(1, args.warmup)):
@@ -200,7 +225,10 @@ def main():
     host_value = None
     if rank == 0 and world == 1 and not args.no_host_entry:
         th = time.perf_counter()
-        _, sh = solver.solve_layers(mine, opts)
+        if offs is not None:
+            _, sh = solver.solve_chains(mine, offs, opts)
+        else:
+            _, sh = solver.solve_layers(mine, opts)
         host_value = int(sh["iterations"].sum()) / (time.perf_counter() - th)
 
     if rank == 0:
@@ -234,14 +262,15 @@ def main():
                        "layers_per_gpu": hi - lo if world == 1 else f"{total // world}-{-(-total // world)}",
                        "layer_iterations_per_step": units_total, "nonconverged_layers": nonconv,
                        "max_rel_error": max_rel, "parallelism": f"layers sharded x{world} (dist.shard_range)",
-                       "init": "boundary_layer", "acceleration": bool(opts.acceleration),
+                       "init": f"warm_chain x{len(offs) - 1} clouds of {args.chain_len} layers" if offs is not None
+                       else "boundary_layer", "acceleration": bool(opts.acceleration),
                        "line_overlap": bool(opts.line_overlap)},
             "roofline": roof,
         }
         if host_value is not None:
             out["host_entry_value"] = host_value
         if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(prob, mine, opts, args.cpu_budget)
+            out["cpu_baseline"] = cpu_baseline(prob, mine, opts, args.cpu_budget, args.chain_len)
         print(json.dumps(out))
     solver.close()
     if multi:

@@ -15,8 +15,9 @@
  * Plain C: no torch or HIP types cross this boundary. Every pointer in the
  * description structs is a HOST pointer that is read during the call only
  * (lvg_create copies all tables to the device; no pointer is retained).
- * The only exception is lvg_solve_layers_device(), whose buffers are device
- * pointers (inputs already resident in HBM).
+ * The exceptions are lvg_solve_layers_device() and lvg_solve_chains_device(),
+ * whose layer/population/status buffers are device pointers (inputs already
+ * resident in HBM).
  *
  * Units are the reference's CGS units: energies in cm^-1, masses in g,
  * concentrations in cm^-3, velocities in cm/s, velocity gradients in s^-1,
@@ -28,7 +29,7 @@
  * in lvg_layer_status (the reference's `bad_layers`, radiative_transfer.cpp:278-288).
  *
  * Threading: one handle per host thread. Every call on a handle is synchronous
- * except lvg_solve_layers_device with a non-NULL stream, which returns once its
+ * except lvg_solve_layers_device / lvg_solve_chains_device with a non-NULL stream, which returns once its
  * kernel is queued; later calls on the same handle are ordered after it (same
  * stream: stream order; any other stream, including the handle's own: the call
  * first waits for it), and the handle frees nothing that kernel uses before it ends.
@@ -89,7 +90,9 @@ enum lvg_init {
     LVG_INIT_GIVEN          = 1,
     /* the reference default (radiative_transfer.cpp:247-252): layer l starts from
      * layer l-1's result when l-1 converged, else from boundary_layer_populations.
-     * Sequential across layers by construction. */
+     * Sequential across the layers of one cloud by construction: one workgroup
+     * (one wave for N <= 64) walks the chain. lvg_solve_chains runs many clouds'
+     * chains in one launch (the reference's OpenMP axis, radiative_transfer.cpp:152-216). */
     LVG_INIT_WARM_CHAIN     = 2
 };
 
@@ -225,10 +228,27 @@ int         lvg_solve_layers(lvg_handle *h, const lvg_layers *layers, double *po
  * oh2_conc, he_conc, mol_conc, vel_turb, vel_grad, then dust_conc[c]) — see
  * lvg_layer_soa_rows(). d_status: [nb_lay] lvg_layer_status. Asynchronous on
  * a non-NULL `stream` (see Threading above); synchronous with NULL.
- * LVG_INIT_WARM_CHAIN is not accepted here (see lvg_solve_chains). */
+ * LVG_INIT_WARM_CHAIN treats the nb_lay layers as one cloud (one chain). */
 int         lvg_layer_soa_rows(const lvg_handle *h);
 int         lvg_solve_layers_device(lvg_handle *h, int nb_lay, const double *d_layer_soa,
                                     double *d_pops_inout, const lvg_solve_opts *opts,
+                                    lvg_layer_status *d_status, void *stream);
+
+/* Batched warm chains: nb_chain independent clouds in ONE launch. The reference
+ * runs calc_molecular_populations (radiative_transfer.cpp:219-289, default start
+ * rule :247-252) once per cloud, one cloud per OpenMP thread (:152-216); here chain
+ * c is layers [chain_off[c], chain_off[c+1]) of `layers`, walked in layer order by
+ * one workgroup (one wave for N <= 64), all chains in parallel (longest first).
+ * Results per chain equal lvg_solve_layers(LVG_INIT_WARM_CHAIN) on that chain alone.
+ * chain_off: HOST [nb_chain + 1], chain_off[0] = 0, non-decreasing,
+ * chain_off[nb_chain] = nb_lay. opts->init must be LVG_INIT_WARM_CHAIN.
+ * pops_out: host [nb_lay*N]; status: host [nb_lay] or NULL. */
+int         lvg_solve_chains(lvg_handle *h, const lvg_layers *layers, int nb_chain, const int *chain_off,
+                             double *pops_out, const lvg_solve_opts *opts, lvg_layer_status *status);
+/* Device-resident variant: d_layer_soa / d_pops_out / d_status as in
+ * lvg_solve_layers_device; chain_off stays a HOST array (copied on `stream`). */
+int         lvg_solve_chains_device(lvg_handle *h, int nb_lay, const double *d_layer_soa, int nb_chain,
+                                    const int *chain_off, double *d_pops_out, const lvg_solve_opts *opts,
                                     lvg_layer_status *d_status, void *stream);
 
 /* One calc_new_pop (iteration_lvg.cpp:87-110) for layer `layer` on the device:

@@ -904,6 +904,48 @@ int oracle_solve_layers(const lvg_problem *P, const lvg_layers *L, double *pops,
     return err ? LVG_E_ARG : LVG_OK;
 }
 
+/* Independent clouds, each a warm chain (radiative_transfer.cpp:219-289 with the
+ * default start rule :247-252): chain c is layers [chain_off[c], chain_off[c+1]),
+ * solved in order; chains run in parallel, one per OpenMP thread, as the reference
+ * runs one shock model per thread (radiative_transfer.cpp:152-216). */
+int oracle_solve_chains(const lvg_problem *P, const lvg_layers *L, int nb_chain, const int *chain_off,
+                        double *pops, const lvg_solve_opts *o, lvg_layer_status *status, int nthreads)
+{
+    int N = P->mol->nb_lev;
+    if (o->init != LVG_INIT_WARM_CHAIN || nb_chain < 1 || chain_off[0] != 0 || chain_off[nb_chain] != L->nb_lay)
+        return LVG_E_ARG;
+    if (o->line_overlap && (!P->overlap1 || !P->overlap2)) return LVG_E_ARG;
+    if (o->accel_nb < 2 || o->accel_nb + 2 > MAX_HIST || (o->acceleration && o->accel_start < o->accel_nb))
+        return LVG_E_ARG;
+    int err = 0;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel num_threads(nthreads) reduction(| : err)
+#endif
+    {
+        scheme_t S; ictl_t C;
+        if (scheme_init(&S, P, o->line_overlap) || ictl_init(&C, N, o->accel_nb)) err = 1;
+        else {
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+            for (int c = 0; c < nb_chain; c++) {
+                int prev_found = 0;
+                for (int l = chain_off[c]; l < chain_off[c + 1]; l++) {
+                    lvg_layer_status st;
+                    solve_one_layer(&S, &C, L, l, pops, NULL, l > chain_off[c] && prev_found, o, &st);
+                    prev_found = st.converged;
+                    if (status) status[l] = st;
+                }
+            }
+            ictl_free(&C);
+        }
+        scheme_free(&S);
+    }
+    (void)N;
+    return err ? LVG_E_ARG : LVG_OK;
+}
+
 int oracle_calc_new_pop(const lvg_problem *P, const lvg_layers *L, int layer, const double *pop_in,
                         int overlap, double *matrix_out, double *df_out, double *pop_out, double *eq_error)
 {

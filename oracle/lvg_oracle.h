@@ -12,6 +12,8 @@ extern "C" {
 void   oracle_opts_default(lvg_solve_opts *o);
 int    oracle_solve_layers(const lvg_problem *P, const lvg_layers *L, double *pops,
                            const lvg_solve_opts *o, lvg_layer_status *status, int nthreads);
+int    oracle_solve_chains(const lvg_problem *P, const lvg_layers *L, int nb_chain, const int *chain_off,
+                           double *pops, const lvg_solve_opts *o, lvg_layer_status *status, int nthreads);
 int    oracle_calc_new_pop(const lvg_problem *P, const lvg_layers *L, int layer, const double *pop_in,
                            int overlap, double *matrix_out, double *df_out, double *pop_out,
                            double *eq_error);

@@ -44,6 +44,7 @@ def lib(ref: bool = False):
         d, i, vp = C.c_double, C.c_int, C.c_void_p
         dp = C.POINTER(C.c_double)
         L.oracle_solve_layers.argtypes = [vp, vp, dp, vp, vp, i]
+        L.oracle_solve_chains.argtypes = [vp, vp, i, C.POINTER(C.c_int), dp, vp, vp, i]
         L.oracle_calc_new_pop.argtypes = [vp, vp, i, dp, i, dp, dp, dp, dp]
         L.oracle_boundary_layer_populations.argtypes = [vp, vp, dp]
         L.oracle_coll_rates.argtypes = [vp, vp, i, dp, dp, dp, dp]
@@ -83,6 +84,20 @@ def solve_layers(prob: abi.Problem, layers: abi.Layers, opts=None, pops=None, nt
                                    st.ctypes.data_as(C.c_void_p), nthreads)
     if rc != 0:
         raise RuntimeError(f"oracle_solve_layers failed: {rc}")
+    return out, st
+
+
+def solve_chains(prob: abi.Problem, layers: abi.Layers, chain_off, opts=None, nthreads: int = 0, ref: bool = False):
+    """oracle_solve_chains: independent warm chains [chain_off[c], chain_off[c+1])."""
+    cp, cl = prob.to_c(), layers.to_c()
+    o = opts if opts is not None else abi.default_opts(init=abi.LVG_INIT_WARM_CHAIN)
+    off = np.ascontiguousarray(chain_off, dtype=np.int32)
+    out = np.zeros((layers.nb_lay, prob.mol.nb_lev))
+    st = np.zeros(layers.nb_lay, dtype=abi.STATUS_DTYPE)
+    rc = lib(ref).oracle_solve_chains(cp.ptr, cl.ptr, len(off) - 1, off.ctypes.data_as(C.POINTER(C.c_int)),
+                                      abi.dptr(out), C.byref(o), st.ctypes.data_as(C.c_void_p), nthreads)
+    if rc != 0:
+        raise RuntimeError(f"oracle_solve_chains failed: {rc}")
     return out, st
 
 

@@ -79,6 +79,10 @@ struct lvg_handle {
     // layer scheduling order (lvg_sched.hip)
     void *d_sched = nullptr, *d_sched_tmp = nullptr;
     size_t sched_cap = 0, sched_tmp_cap = 0;
+    // warm chains: offsets [nb_chain + 1] then queue order [nb_chain] (device + host staging)
+    int *d_chain = nullptr;
+    size_t chain_cap = 0;
+    std::vector<int> chain_host;
     double last_ms = 0.;
     int last_launches = 0;
     // an asynchronous lvg_solve_layers_device (caller's stream) may still be running:
@@ -666,6 +670,7 @@ void lvg_destroy(lvg_handle *h) {
     if (h->d_launch) (void)hipFree(h->d_launch);
     if (h->d_sched) (void)hipFree(h->d_sched);
     if (h->d_sched_tmp) (void)hipFree(h->d_sched_tmp);
+    if (h->d_chain) (void)hipFree(h->d_chain);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -716,19 +721,31 @@ int lvg_create(const lvg_problem *prob, int device, lvg_handle **out) {
     return LVG_OK;
 }
 
-int lvg_solve_layers_device(lvg_handle *h, int nb_lay, const double *d_soa, double *d_pops,
-                            const lvg_solve_opts *o, lvg_layer_status *d_status, void *stream) {
-    if (!h) return LVG_E_STATE;
-    int rc = check_opts(h, o);
-    if (rc) return rc;
-    if (o->init == LVG_INIT_WARM_CHAIN) return fail(h, LVG_E_ARG, "warm chain is only available through lvg_solve_layers");
-    if (nb_lay < 0 || (nb_lay > 0 && (!d_soa || !d_pops || !d_status))) return fail(h, LVG_E_ARG, "bad device buffers");
+}  // extern "C"
+
+namespace {
+
+// chain_off: host [nb_chain + 1] (warm chains) or NULL (independent layers)
+int check_chains(lvg_handle *h, int nb_lay, int nb_chain, const int *chain_off) {
+    if (nb_chain < 1 || !chain_off) return fail(h, LVG_E_ARG, "warm chains need nb_chain >= 1 and chain_off");
+    if (chain_off[0] != 0 || chain_off[nb_chain] != nb_lay)
+        return fail(h, LVG_E_ARG, "chain_off must start at 0 and end at nb_lay");
+    for (int c = 0; c < nb_chain; c++)
+        if (chain_off[c + 1] < chain_off[c]) return fail(h, LVG_E_ARG, "chain_off must be non-decreasing");
+    return LVG_OK;
+}
+
+// One persistent launch over device-resident buffers (caller has validated arguments).
+int launch_solve(lvg_handle *h, int nb_lay, const double *d_soa, double *d_pops, const lvg_solve_opts *o,
+                 lvg_layer_status *d_status, void *stream, int nb_chain, const int *chain_off) {
+    int rc;
     h->last_ms = 0.;
     h->last_launches = 0;
     if (nb_lay == 0) return LVG_OK;
     HIPCHECK(h, hipSetDevice(h->device));
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     settle(h, s);
+    const int nq = chain_off ? nb_chain : nb_lay;   // queue items
     int per_cu = h->blocks_per_cu;
     if (const char *e = std::getenv("LVG_BLOCKS_PER_CU")) {   // tuning/diagnostics only
         const int v = std::atoi(e);
@@ -750,8 +767,8 @@ int lvg_solve_layers_device(lvg_handle *h, int nb_lay, const double *d_soa, doub
         }
     }
     const bool wave = wpb > 0;
-    const int grid = wave ? std::max(1, std::min((nb_lay + wpb - 1) / wpb, h->cus * wave_bpc))
-                          : std::max(1, std::min(nb_lay, h->cus * per_cu));
+    const int grid = wave ? std::max(1, std::min((nq + wpb - 1) / wpb, h->cus * wave_bpc))
+                          : std::max(1, std::min(nq, h->cus * per_cu));
     const int slots = wave ? grid * wpb : grid;
     h->last_kernel = wave ? 1 : 0;
     if ((rc = ensure_workspace(h, slots))) return rc;
@@ -763,7 +780,24 @@ int lvg_solve_layers_device(lvg_handle *h, int nb_lay, const double *d_soa, doub
     L.soa = d_soa;
     L.pops = d_pops;
     L.status = d_status;
-    if (nb_lay > slots && !std::getenv("LVG_INDEX_ORDER")) {
+    if (chain_off) {
+        // chains: offsets, then the queue in decreasing chain length (stable; results do
+        // not depend on the order, each chain is computed on its own)
+        auto &hc = h->chain_host;
+        drain(h);   // the staging vector may still feed an earlier asynchronous copy
+        hc.assign(chain_off, chain_off + nb_chain + 1);
+        std::vector<int> ord(nb_chain);
+        for (int c = 0; c < nb_chain; c++) ord[c] = c;
+        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
+            return chain_off[a + 1] - chain_off[a] > chain_off[b + 1] - chain_off[b];
+        });
+        hc.insert(hc.end(), ord.begin(), ord.end());
+        if ((rc = grow(h, (void **)&h->d_chain, &h->chain_cap, sizeof(int) * hc.size()))) return rc;
+        HIPCHECK(h, hipMemcpyAsync(h->d_chain, hc.data(), sizeof(int) * hc.size(), hipMemcpyHostToDevice, s));
+        L.chain_off = h->d_chain;
+        L.nb_chain = nb_chain;
+        L.order = h->d_chain + nb_chain + 1;
+    } else if (nb_lay > slots && !std::getenv("LVG_INDEX_ORDER")) {
         // longest-expected-first order of the work queue (lvg_sched.hip); results do not
         // depend on it. Scratch: keys, sorted keys (double), indices, order (int).
         size_t tmp = 0;
@@ -794,6 +828,34 @@ int lvg_solve_layers_device(lvg_handle *h, int nb_lay, const double *d_soa, doub
         h->pending_stream = s;
     }
     return LVG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lvg_solve_layers_device(lvg_handle *h, int nb_lay, const double *d_soa, double *d_pops,
+                            const lvg_solve_opts *o, lvg_layer_status *d_status, void *stream) {
+    if (!h) return LVG_E_STATE;
+    int rc = check_opts(h, o);
+    if (rc) return rc;
+    if (nb_lay < 0 || (nb_lay > 0 && (!d_soa || !d_pops || !d_status))) return fail(h, LVG_E_ARG, "bad device buffers");
+    if (o->init == LVG_INIT_WARM_CHAIN) {   // one chain over all layers
+        const int off[2] = {0, nb_lay};
+        return launch_solve(h, nb_lay, d_soa, d_pops, o, d_status, stream, 1, nb_lay ? off : nullptr);
+    }
+    return launch_solve(h, nb_lay, d_soa, d_pops, o, d_status, stream, 0, nullptr);
+}
+
+int lvg_solve_chains_device(lvg_handle *h, int nb_lay, const double *d_soa, int nb_chain, const int *chain_off,
+                            double *d_pops, const lvg_solve_opts *o, lvg_layer_status *d_status, void *stream) {
+    if (!h) return LVG_E_STATE;
+    int rc = check_opts(h, o);
+    if (rc) return rc;
+    if (o->init != LVG_INIT_WARM_CHAIN) return fail(h, LVG_E_ARG, "lvg_solve_chains needs init = LVG_INIT_WARM_CHAIN");
+    if (nb_lay < 0 || (nb_lay > 0 && (!d_soa || !d_pops || !d_status))) return fail(h, LVG_E_ARG, "bad device buffers");
+    if ((rc = check_chains(h, nb_lay, nb_chain, chain_off))) return rc;
+    return launch_solve(h, nb_lay, d_soa, d_pops, o, d_status, stream, nb_chain, chain_off);
 }
 
 int lvg_last_kernel_time(const lvg_handle *h, double *ms, int *nb) {
@@ -828,63 +890,58 @@ static int upload_layers(lvg_handle *h, const lvg_layers *L) {
     return LVG_OK;
 }
 
-int lvg_solve_layers(lvg_handle *h, const lvg_layers *layers, double *pops, const lvg_solve_opts *o,
-                     lvg_layer_status *status) {
-    if (!h) return LVG_E_STATE;
-    if (!layers || (layers->nb_lay > 0 && !pops)) return fail(h, LVG_E_ARG, "layers / pops missing");
-    int rc = check_opts(h, o);
-    if (rc) return rc;
+}  // extern "C"
+
+namespace {
+
+// host-buffer solve: upload the layer SoA (and given populations), one launch, copy back
+int solve_host(lvg_handle *h, const lvg_layers *layers, double *pops, const lvg_solve_opts *o,
+               lvg_layer_status *status, int nb_chain, const int *chain_off) {
     const int nl = layers->nb_lay, N = h->N;
+    int rc;
     if (nl == 0) return LVG_OK;
     HIPCHECK(h, hipSetDevice(h->device));
     settle(h, h->stream);
     if ((rc = upload_layers(h, layers))) return rc;
     if ((rc = grow(h, (void **)&h->d_pops, &h->pops_cap, sizeof(double) * (size_t)nl * N))) return rc;
     if ((rc = grow(h, &h->d_status, &h->status_cap, sizeof(lvg_layer_status) * (size_t)nl))) return rc;
-    if (o->init != LVG_INIT_BOUNDARY_LAYER)
+    if (o->init == LVG_INIT_GIVEN)
         HIPCHECK(h, hipMemcpyAsync(h->d_pops, pops, sizeof(double) * (size_t)nl * N, hipMemcpyHostToDevice, h->stream));
-    if (o->init == LVG_INIT_WARM_CHAIN) {
-        // the reference default: sequential chain, one layer per launch
-        if ((rc = ensure_workspace(h, 1))) return rc;
-        LvgLaunch L;
-        fill_launch(h, L, o);
-        L.soa = h->d_soa;
-        L.soa_ld = nl;
-        L.nb_lay = 1;
-        L.chain = 1;
-        std::vector<const LvgLaunch *> dls(nl);
-        for (int l = 0; l < nl; l++) {
-            L.lay_offset = l;
-            L.pops = h->d_pops + (size_t)l * N;
-            L.status = (lvg_layer_status *)h->d_status + l;
-            if ((rc = push_launch(h, L, l, h->stream, &dls[l]))) return rc;
-        }
-        for (int l = 0; l < nl; l++) dls[l] = h->d_launch + l;   // the block may have been reallocated
-        for (int l = 0; l < nl; l++) {
-            L.lay_offset = l;
-            L.pops = h->d_pops + (size_t)l * N;
-            L.status = (lvg_layer_status *)h->d_status + l;
-            HIPCHECK(h, hipMemcpyAsync(h->d_launch + l, &L, sizeof L, hipMemcpyHostToDevice, h->stream));
-        }
-        HIPCHECK(h, hipStreamSynchronize(h->stream));
-        HIPCHECK(h, hipEventRecord(h->ev0, h->stream));
-        for (int l = 0; l < nl; l++) {
-            HIPCHECK(h, hipMemsetAsync(h->counter, 0, sizeof(int), h->stream));
-            HIPCHECK(h, lvg_launch_solve(h->d_prob, dls[l], 1, h->stream));
-        }
-        HIPCHECK(h, hipEventRecord(h->ev1, h->stream));
-        HIPCHECK(h, hipStreamSynchronize(h->stream));
-        float ms = 0.f;
-        (void)hipEventElapsedTime(&ms, h->ev0, h->ev1);
-        h->last_ms = ms;
-        h->last_launches = nl;
-    } else {
-        rc = lvg_solve_layers_device(h, nl, h->d_soa, h->d_pops, o, (lvg_layer_status *)h->d_status, nullptr);
-        if (rc) return rc;
-    }
+    rc = launch_solve(h, nl, h->d_soa, h->d_pops, o, (lvg_layer_status *)h->d_status, nullptr, nb_chain, chain_off);
+    if (rc) return rc;
     HIPCHECK(h, hipMemcpy(pops, h->d_pops, sizeof(double) * (size_t)nl * N, hipMemcpyDeviceToHost));
     if (status) HIPCHECK(h, hipMemcpy(status, h->d_status, sizeof(lvg_layer_status) * (size_t)nl, hipMemcpyDeviceToHost));
     return LVG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lvg_solve_layers(lvg_handle *h, const lvg_layers *layers, double *pops, const lvg_solve_opts *o,
+                     lvg_layer_status *status) {
+    if (!h) return LVG_E_STATE;
+    if (!layers || (layers->nb_lay > 0 && !pops)) return fail(h, LVG_E_ARG, "layers / pops missing");
+    int rc = check_opts(h, o);
+    if (rc) return rc;
+    const int nl = layers->nb_lay;
+    if (o->init == LVG_INIT_WARM_CHAIN) {
+        // the reference default (radiative_transfer.cpp:247-252): one chain over the cloud
+        const int off[2] = {0, nl};
+        return solve_host(h, layers, pops, o, status, 1, off);
+    }
+    return solve_host(h, layers, pops, o, status, 0, nullptr);
+}
+
+int lvg_solve_chains(lvg_handle *h, const lvg_layers *layers, int nb_chain, const int *chain_off, double *pops,
+                     const lvg_solve_opts *o, lvg_layer_status *status) {
+    if (!h) return LVG_E_STATE;
+    if (!layers || (layers->nb_lay > 0 && !pops)) return fail(h, LVG_E_ARG, "layers / pops missing");
+    int rc = check_opts(h, o);
+    if (rc) return rc;
+    if (o->init != LVG_INIT_WARM_CHAIN) return fail(h, LVG_E_ARG, "lvg_solve_chains needs init = LVG_INIT_WARM_CHAIN");
+    if ((rc = check_chains(h, layers->nb_lay, nb_chain, chain_off))) return rc;
+    return solve_host(h, layers, pops, o, status, nb_chain, chain_off);
 }
 
 int lvg_debug_calc_new_pop(lvg_handle *h, const lvg_layers *layers, int layer, const double *pop_in, int line_overlap,

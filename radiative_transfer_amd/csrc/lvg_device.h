@@ -84,7 +84,11 @@ struct LvgLaunch {
     double        min_error;
     int max_iter_acc, max_iter_plain, accel_start, accel_period, accel_nb;
     int acceleration, allow_plain_retry, init, line_overlap;
-    int chain;                        // warm-chain launch: layer lay_offset uses pops/status of lay_offset-1
+    // warm chains (LVG_INIT_WARM_CHAIN): queue items are chains, chain c is layers
+    // [chain_off[c], chain_off[c+1]) solved in order by one workgroup / wave, each layer
+    // starting from its predecessor when that converged (radiative_transfer.cpp:247-252)
+    const int *chain_off;             // [nb_chain + 1], NULL: queue items are layers
+    int nb_chain;
     // workspace (per resident block slot)
     double   *ws;                     // [nb_slots][ws_stride]
     int64_t   ws_stride;

@@ -1827,8 +1827,10 @@ __device__ __forceinline__ Slot make_slot(const LvgDevProblem &P, const LvgLaunc
     return S;
 }
 
-// One layer of calc_molecular_populations (radiative_transfer.cpp:236-288).
-__device__ __forceinline__ void solve_layer(const LvgDevProblem &P, const LvgLaunch &Lc, int l, Slot &S, Smem &sm) {
+// One layer of calc_molecular_populations (radiative_transfer.cpp:236-288). from_prev:
+// warm chain and the previous layer of the chain converged (:247-249). Returns is_found.
+__device__ __forceinline__ bool solve_layer(const LvgDevProblem &P, const LvgLaunch &Lc, int l, Slot &S, Smem &sm,
+                                            bool from_prev) {
     const int N = P.N, t = threadIdx.x;
     const LvgModeLines &M = Lc.line_overlap ? P.overlap : P.plain;
     TSTAMP(ts0);
@@ -1838,15 +1840,11 @@ __device__ __forceinline__ void solve_layer(const LvgDevProblem &P, const LvgLau
     double *pops = Lc.pops + (int64_t)l * N;
     lvg_layer_status *st = reinterpret_cast<lvg_layer_status *>(Lc.status) + l;
     const bool need_boundary = (Lc.init != LVG_INIT_GIVEN);
-    build_collision_operators(P, sm, S.K, need_boundary ? S.A : nullptr);
+    build_collision_operators(P, sm, S.K, (need_boundary && !from_prev) ? S.A : nullptr);
     TACC(PH_SETUP, ts0);
 
-    // initial guess (radiative_transfer.cpp:247-252)
-    bool from_prev = false;
-    if (Lc.init == LVG_INIT_WARM_CHAIN && Lc.chain && (Lc.lay_offset + l) > 0) {
-        const lvg_layer_status *ps = reinterpret_cast<const lvg_layer_status *>(Lc.status) + l - 1;
-        from_prev = ps->converged != 0;
-    }
+    // initial guess (radiative_transfer.cpp:247-252); the previous layer's populations
+    // were written by this same thread (same level index), so they are visible here
     if (Lc.init == LVG_INIT_GIVEN) {
         for (int i = t; i < N; i += BT) { sm.pold[i] = pops[i]; S.given[i] = pops[i]; }
         __syncthreads();
@@ -1888,7 +1886,7 @@ __device__ __forceinline__ void solve_layer(const LvgDevProblem &P, const LvgLau
             __syncthreads();
             if (Lc.dbg_mode == 2) {
                 for (int i = t; i < N; i += BT) pops[i] = sm.pold[i];
-                return;
+                return false;
             }
             boundary = false;
             start_pass(C, P, S, Lc, accel ? Lc.max_iter_acc : Lc.max_iter_plain, accel);
@@ -1922,8 +1920,11 @@ __device__ __forceinline__ void solve_layer(const LvgDevProblem &P, const LvgLau
     TACC(PH_CLK_MEMTIME, ts0);
     RACC(PH_CLK_REALTIME, rs0);
     __syncthreads();
+    return found;
 }
 
+// Persistent: workgroups pull queue items (layers, or whole warm chains) from an atomic
+// counter; `order` maps queue positions to items (longest expected first).
 __global__ void __launch_bounds__(BT, LVG_OCC) solve_kernel(const LvgDevProblem *__restrict__ Pp,
                                                        const LvgLaunch *__restrict__ Lp) {
     __shared__ Smem sm;
@@ -1932,17 +1933,25 @@ __global__ void __launch_bounds__(BT, LVG_OCC) solve_kernel(const LvgDevProblem 
     PH_INIT();
     load_rule_table(P, sm);
     Slot S = make_slot(P, Lc, blockIdx.x);
+    const int nq = Lc.chain_off ? Lc.nb_chain : Lc.nb_lay;
     for (;;) {
         if (threadIdx.x == 0) {
             const int q = atomicAdd(Lc.counter, 1);
-            sm.layer = (q < Lc.nb_lay && Lc.order) ? Lc.order[q] : q;
+            sm.layer = (q < nq && Lc.order) ? Lc.order[q] : q;
             sm.pidx = q;
         }
         __syncthreads();
         const int l = sm.layer, q = sm.pidx;
         __syncthreads();
-        if (q >= Lc.nb_lay) break;
-        solve_layer(P, Lc, l, S, sm);
+        if (q >= nq) break;
+        if (!Lc.chain_off) {
+            solve_layer(P, Lc, l, S, sm, false);
+        } else {
+            // warm chain l: layers in order, each from its predecessor if that converged
+            const int lo = Lc.chain_off[l], hi = Lc.chain_off[l + 1];
+            bool prev = false;
+            for (int k = lo; k < hi; k++) prev = solve_layer(P, Lc, k, S, sm, k > lo && prev);
+        }
     }
     PH_FLUSH();
 }

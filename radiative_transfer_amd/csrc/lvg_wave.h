@@ -516,10 +516,11 @@ __device__ __forceinline__ void wave_next_step_post(Ctl &C, Slot &S, int N, Wave
 }
 
 // One layer of calc_molecular_populations (radiative_transfer.cpp:236-288), one wave.
+// from_prev: warm chain and the chain's previous layer converged (:247-249). Returns is_found.
 template <int NM>
-__device__ __forceinline__ void wave_solve_layer(const LvgDevProblem &P, const LvgLaunch &Lc, const WaveShared &sh,
+__device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const LvgLaunch &Lc, const WaveShared &sh,
                                                  WaveLayer &sm, const EscGrids &G, const int *li, int ldk, double *K,
-                                                 Slot &S, int l) {
+                                                 Slot &S, int l, bool from_prev) {
     const int N = P.N, t = lane_id();
     const LvgModeLines &M = Lc.line_overlap ? P.overlap : P.plain;
     TSTAMP(ts0);
@@ -528,16 +529,20 @@ __device__ __forceinline__ void wave_solve_layer(const LvgDevProblem &P, const L
     double *pops = Lc.pops + (int64_t)l * N;
     lvg_layer_status *st = reinterpret_cast<lvg_layer_status *>(Lc.status) + l;
     const bool need_boundary = (Lc.init != LVG_INIT_GIVEN);
-    wave_collisions(P, sh, sm, K, ldk, need_boundary ? S.A : nullptr);
+    wave_collisions(P, sh, sm, K, ldk, (need_boundary && !from_prev) ? S.A : nullptr);
     wave_sync();
     TACC(PH_SETUP, ts0);
     if (!need_boundary) {
         if (t < N) { sm.pold[t] = pops[t]; S.given[t] = pops[t]; }
         wave_sync();
+    } else if (from_prev) {
+        // the previous layer's populations were stored by this same lane
+        if (t < N) { sm.pold[t] = pops[t - N]; S.given[t] = pops[t - N]; }
+        wave_sync();
     }
     Ctl C;
     const int accel = Lc.acceleration;
-    bool boundary = need_boundary, found = false;
+    bool boundary = need_boundary && !from_prev, found = false;
     int iters = 0, retry = 0;
     const int row = t < N ? t : 0;
     if (!boundary) wave_start_pass(C, S, Lc, N, accel ? Lc.max_iter_acc : Lc.max_iter_plain, accel);
@@ -603,7 +608,7 @@ __device__ __forceinline__ void wave_solve_layer(const LvgDevProblem &P, const L
             wave_sync();
             if (Lc.dbg_mode == 2) {
                 if (t < N) pops[t] = sm.pold[t];
-                return;
+                return false;
             }
             boundary = false;
             wave_start_pass(C, S, Lc, N, accel ? Lc.max_iter_acc : Lc.max_iter_plain, accel);
@@ -635,6 +640,7 @@ __device__ __forceinline__ void wave_solve_layer(const LvgDevProblem &P, const L
         st->pop_error = C.pop_error;
     }
     wave_sync();
+    return found;
 }
 
 template <int NM>
@@ -680,13 +686,21 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
     const EscGrids G{sh.grids, sh.grids + o1, sh.grids + o2, sh.grids + o3, sh.grids + o4, sh.grids + o5};
     WaveLayer &sm = sh.w[w];
     Slot S = make_slot(P, Lc, blockIdx.x * wpb + w);
+    const int nq = Lc.chain_off ? Lc.nb_chain : Lc.nb_lay;
     for (;;) {
         int q = 0;
         if (lane_id() == 0) q = atomicAdd(Lc.counter, 1);
         q = __builtin_amdgcn_readfirstlane(q);
-        if (q >= Lc.nb_lay) break;
+        if (q >= nq) break;
         const int l = Lc.order ? Lc.order[q] : q;
-        wave_solve_layer<NM>(P, Lc, sh, sm, G, li, ldk, K, S, l);
+        if (!Lc.chain_off) {
+            wave_solve_layer<NM>(P, Lc, sh, sm, G, li, ldk, K, S, l, false);
+        } else {
+            // warm chain l, in layer order (one wave per chain)
+            const int lo = Lc.chain_off[l], hi = Lc.chain_off[l + 1];
+            bool prev = false;
+            for (int k = lo; k < hi; k++) prev = wave_solve_layer<NM>(P, Lc, sh, sm, G, li, ldk, K, S, k, k > lo && prev);
+        }
     }
     PH_FLUSH();
 }

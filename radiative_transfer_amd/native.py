@@ -20,7 +20,8 @@ LIB_PATH = os.environ.get("LVG_LIB_PATH") or os.path.join(_PKG, "_lib", "liblvg_
 EXPORTS = ("lvg_abi_version", "lvg_solve_opts_default", "lvg_create", "lvg_destroy", "lvg_last_error",
            "lvg_nb_lev", "lvg_solve_layers", "lvg_layer_soa_rows", "lvg_solve_layers_device",
            "lvg_debug_calc_new_pop", "lvg_boundary_layer_populations", "lvg_find_opts_default",
-           "lvg_find_transitions", "lvg_lim_luminosity", "lvg_last_kernel_time")
+           "lvg_find_transitions", "lvg_lim_luminosity", "lvg_last_kernel_time", "lvg_solve_chains",
+           "lvg_solve_chains_device")
 
 _lib = None
 
@@ -48,6 +49,8 @@ def load(path: str = LIB_PATH):
     L.lvg_solve_layers.argtypes = [vp, vp, dp, vp, vp]
     L.lvg_layer_soa_rows.argtypes = [vp]
     L.lvg_solve_layers_device.argtypes = [vp, i, vp, vp, vp, vp, vp]
+    L.lvg_solve_chains.argtypes = [vp, vp, i, C.POINTER(C.c_int), dp, vp, vp]
+    L.lvg_solve_chains_device.argtypes = [vp, i, vp, i, C.POINTER(C.c_int), vp, vp, vp, vp]
     L.lvg_debug_calc_new_pop.argtypes = [vp, vp, i, dp, i, dp, dp, dp, dp]
     L.lvg_boundary_layer_populations.argtypes = [vp, vp, dp]
     L.lvg_last_kernel_time.argtypes = [vp, dp, C.POINTER(C.c_int)]
@@ -101,6 +104,30 @@ class LvgSolver:
         rc = self.lib.lvg_solve_layers(self.h, cl.ptr, abi.dptr(out), C.byref(o), st.ctypes.data_as(C.c_void_p))
         self._check(rc, "lvg_solve_layers")
         return out, st
+
+    def solve_chains(self, layers: abi.Layers, chain_off, opts=None):
+        """Independent clouds, each a warm chain (layers [chain_off[c], chain_off[c+1])),
+        in one launch -> (pops [L,N], status). opts.init must be LVG_INIT_WARM_CHAIN."""
+        o = opts if opts is not None else abi.default_opts(init=abi.LVG_INIT_WARM_CHAIN)
+        cl = layers.to_c()
+        off = np.ascontiguousarray(chain_off, dtype=np.int32)
+        out = np.zeros((layers.nb_lay, self.N))
+        st = np.zeros(layers.nb_lay, dtype=abi.STATUS_DTYPE)
+        rc = self.lib.lvg_solve_chains(self.h, cl.ptr, len(off) - 1, off.ctypes.data_as(C.POINTER(C.c_int)),
+                                       abi.dptr(out), C.byref(o), st.ctypes.data_as(C.c_void_p))
+        self._check(rc, "lvg_solve_chains")
+        return out, st
+
+    def solve_chains_device(self, nb_lay: int, soa_ptr: int, chain_off, pops_ptr: int, status_ptr: int,
+                            opts=None, stream_ptr: int = 0):
+        """Device-resident warm chains; chain_off is a host int array [nb_chain + 1]."""
+        o = opts if opts is not None else abi.default_opts(init=abi.LVG_INIT_WARM_CHAIN)
+        off = np.ascontiguousarray(chain_off, dtype=np.int32)
+        rc = self.lib.lvg_solve_chains_device(self.h, nb_lay, C.c_void_p(soa_ptr), len(off) - 1,
+                                              off.ctypes.data_as(C.POINTER(C.c_int)), C.c_void_p(pops_ptr),
+                                              C.byref(o), C.c_void_p(status_ptr),
+                                              C.c_void_p(stream_ptr) if stream_ptr else None)
+        self._check(rc, "lvg_solve_chains_device")
 
     def soa_rows(self) -> int:
         return self.lib.lvg_layer_soa_rows(self.h)

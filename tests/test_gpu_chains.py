@@ -1,0 +1,89 @@
+"""GPU parity of batched warm chains (lvg_solve_chains). Tolerance:
+none — populations and every status field are bitwise identical to the oracle.
+
+The reference solves one cloud per calc_molecular_populations call with the default
+start rule (radiative_transfer.cpp:247-252: layer l starts from layer l-1's converged
+populations, else from boundary_layer_populations) and runs clouds in parallel, one per
+OpenMP thread (:152-216). lvg_solve_chains takes many clouds at once, one workgroup
+(block kernel) or one wave (N <= 64) per chain; oracle_solve_chains is the checker, and
+tests/test_chains_cpu.py pins it against per-cloud oracle_solve_layers(WARM_CHAIN).
+"""
+import numpy as np
+import pytest
+
+from radiative_transfer_amd import abi, synth
+from radiative_transfer_amd.native import LvgError, LvgSolver
+from oracle import oracle
+from parity_helpers import assert_same, env
+
+pytestmark = pytest.mark.gpu
+
+WARM = abi.LVG_INIT_WARM_CHAIN
+
+
+def _cmp_chains(s, P, L, off, opts):
+    pg, sg = s.solve_chains(L, off, opts)
+    po, so = oracle.solve_chains(P, L, off, opts)
+    assert_same(pg, sg, po, so)
+    return po, so
+
+
+@pytest.mark.parametrize("name,nl,force_block", [("ph2o45_1024", 40, False), ("ph2o45_1024", 14, True),
+                                                 ("oh24_overlap_2048", 24, False), ("ch3oha256_4096", 9, False)])
+def test_chains_bit_exact(name, nl, force_block):
+    P, L, o = synth.make_problem(name, nb_lay=nl)
+    s = LvgSolver(P)
+    # ragged chains, an empty one, a single-layer one
+    cuts = sorted({0, nl, 1, nl // 3, nl // 3, (2 * nl) // 3})
+    off = np.array(cuts + ([nl] if cuts[-1] != nl else []), dtype=np.int32)
+    off = np.concatenate([off[:2], off[1:2], off[2:]])            # duplicate offset: empty chain
+    with env(LVG_BLOCK_KERNEL="1" if force_block else None):
+        po, so = _cmp_chains(s, P, L, off, abi.default_opts(init=WARM, **o))
+        # caps that leave layers unconverged mid-chain: the next layer restarts from the
+        # boundary populations (the is_solution_found_prev branch)
+        kw = {"max_iter_acc": 3, "allow_plain_retry": 0} if o.get("acceleration", 1) else {"max_iter_plain": 3}
+        po, so = _cmp_chains(s, P, L, off, abi.default_opts(init=WARM, **{**o, **kw}))
+        assert (so["converged"] == 0).any() and (so["converged"] == 1).any()
+    s.close()
+
+
+def test_single_chain_equals_warm_chain_solve():
+    """lvg_solve_layers(WARM_CHAIN) is one chain over the cloud."""
+    P, L, o = synth.make_problem("ph2o45_1024", nb_lay=20)
+    s = LvgSolver(P)
+    opts = abi.default_opts(init=WARM, **o)
+    pw, sw = s.solve_layers(L, opts)
+    pc, sc = s.solve_chains(L, [0, L.nb_lay], opts)
+    assert_same(pw, sw, pc, sc)
+    po, so = oracle.solve_layers(P, L, opts)
+    assert_same(pw, sw, po, so)
+    ms, n = s.last_kernel_time()
+    assert ms > 0 and n == 1
+    s.close()
+
+
+def test_chains_device_entry_and_errors():
+    import torch
+    P, L, o = synth.make_problem("ch3oha256_4096", nb_lay=8)
+    s = LvgSolver(P)
+    opts = abi.default_opts(init=WARM, **o)
+    off = [0, 3, 8]
+    ph, sh = s.solve_chains(L, off, opts)
+    dev = torch.device("cuda", 0)
+    soa = torch.from_numpy(L.soa()).to(dev)
+    pops = torch.zeros((L.nb_lay, P.mol.nb_lev), dtype=torch.float64, device=dev)
+    st = torch.zeros((L.nb_lay, abi.STATUS_DTYPE.itemsize // 8), dtype=torch.float64, device=dev)
+    s.solve_chains_device(L.nb_lay, soa.data_ptr(), off, pops.data_ptr(), st.data_ptr(), opts,
+                          stream_ptr=torch.cuda.current_stream().cuda_stream)
+    # a host-entry call right after the asynchronous launch is ordered after it
+    p2, s2 = s.solve_chains(L, off, opts)
+    torch.cuda.synchronize()
+    assert np.array_equal(pops.cpu().numpy(), ph) and np.array_equal(p2, ph)
+    sd = np.frombuffer(st.cpu().numpy().tobytes(), dtype=abi.STATUS_DTYPE)
+    assert np.array_equal(sd, sh) and np.array_equal(s2, sh)
+    for bad in ([1, 8], [0, 9], [0, 5, 3, 8], [0]):
+        with pytest.raises(LvgError):
+            s.solve_chains(L, bad, opts)
+    with pytest.raises(LvgError):
+        s.solve_chains(L, off, abi.default_opts(**o))        # init must be WARM_CHAIN
+    s.close()
