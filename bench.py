@@ -144,6 +144,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="ch3oha256_4096")
     ap.add_argument("--layers", type=int, default=0, help="cloud layers (default: the config's)")
+    ap.add_argument("--nb-lev", type=int, default=0, help="levels (default: the config's; 768 = reference CH3OH)")
     ap.add_argument("--weak", action="store_true", help="config's layers PER GPU instead of one cloud")
     ap.add_argument("--chain-len", type=int, default=0,
                     help="warm chains of this many layers (LVG_INIT_WARM_CHAIN) instead of independent layers")
@@ -169,9 +170,10 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     kind, N, L_cfg, seed = synth.CONFIGS[args.workload]
+    N = args.nb_lev or N
     L_cloud = args.layers or L_cfg
     total = L_cloud * world if args.weak else L_cloud
-    prob, layers_all, o = synth.make_problem(args.workload, nb_lay=total)
+    prob, layers_all, o = synth.make_problem(args.workload, nb_lay=total, nb_lev=N)
     opts = abi.default_opts(**o)
     if args.chain_len:
         opts.init = abi.LVG_INIT_WARM_CHAIN
@@ -234,10 +236,12 @@ def main():
     if rank == 0:
         value = units_total * args.steps / elapsed
         kms = float(np.mean(kern_ms))
-        kernel = "lvg::solve_kernel" if N > 64 else "lvg::solve_wave_kernel"
+        kernel = "lvg::solve_wave_kernel" if N <= 64 else "lvg::solve_kernel" if N <= 256 else "lvg_big::solve_kernel"
         bound = binding_roof(N)
         per_launch = units_local
-        traffic, tsrc = load_pmc_traffic(args.workload)
+        # committed PMC traffic applies only to the profiled configuration
+        traffic, tsrc = load_pmc_traffic(args.workload) if (N, total) == (synth.CONFIGS[args.workload][1],
+                                                                           L_cfg) and not args.chain_len else (None, None)
         if bound == "fp64":
             achieved = flops_per_layer_iteration(N) * per_launch / (kms * 1e-3) / 1e12
             roof = {"bound": "fp64", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",

@@ -15,8 +15,8 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "_lib")
 LIB = os.path.join(LIB_DIR, "liblvg_amd.so")
-SOURCES = ["lvg_kernels.hip", "lvg_transitions.hip", "lvg_sched.hip", "lvg_abi.cpp"]
-HEADERS = ["lvg_device.h", "lvg_wave.h", os.path.join("..", "..", "include", "lvg_amd.h"),
+SOURCES = ["lvg_kernels.hip", "lvg_kernels_big.hip", "lvg_transitions.hip", "lvg_sched.hip", "lvg_abi.cpp"]
+HEADERS = ["lvg_device.h", "lvg_wave.h", "lvg_kernels.hip", os.path.join("..", "..", "include", "lvg_amd.h"),
            os.path.join("..", "..", "include", "lvg_math.h")]
 ARCH = os.environ.get("LVG_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -31,12 +31,25 @@ def _stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile every source to an object in parallel (hipcc per file), then link."""
     if not force and not _stale():
         return LIB
-    os.makedirs(LIB_DIR, exist_ok=True)
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-           "-Wall", "-Wno-unused-function", "-o", LIB + ".tmp"]
-    cmd += [os.path.join(CSRC, f) for f in SOURCES]
+    from concurrent.futures import ThreadPoolExecutor
+    obj_dir = os.path.join(LIB_DIR, "obj")
+    os.makedirs(obj_dir, exist_ok=True)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall",
+             "-Wno-unused-function"]
+    objs = [os.path.join(obj_dir, os.path.splitext(f)[0] + ".o") for f in SOURCES]
+
+    def compile_one(i):
+        cmd = [HIPCC] + flags + ["-c", os.path.join(CSRC, SOURCES[i]), "-o", objs[i]]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+
+    with ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 1)) as ex:
+        list(ex.map(compile_one, range(len(SOURCES))))
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)

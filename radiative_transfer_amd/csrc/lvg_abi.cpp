@@ -34,6 +34,13 @@ extern "C" int lvg_kernel_max_levels(void);
 extern "C" hipError_t lvg_kernel_occupancy(int *blocks_per_cu);
 extern "C" hipError_t lvg_launch_lum(const LvgDevProblem *P, const LvgLaunch *L, const LvgLumArgs *A, int grid,
                                      int nb_trans, int nb_lay, hipStream_t s);
+// the 768-thread instantiation for 256 < N <= 768 (lvg_kernels_big.hip)
+extern "C" hipError_t lvg_launch_solve_big(const LvgDevProblem *P, const LvgLaunch *L, int grid, hipStream_t s);
+extern "C" hipError_t lvg_launch_debug_big(const LvgDevProblem *P, const LvgLaunch *L, hipStream_t s);
+extern "C" int lvg_kernel_max_levels_big(void);
+extern "C" hipError_t lvg_kernel_occupancy_big(int *blocks_per_cu);
+extern "C" hipError_t lvg_launch_lum_big(const LvgDevProblem *P, const LvgLaunch *L, const LvgLumArgs *A, int grid,
+                                         int nb_trans, int nb_lay, hipStream_t s);
 extern "C" hipError_t lvg_sched_order(const double *soa, int ld, int n, double *keys, double *keys_sorted, int *idx,
                                       int *order, void *temp, size_t *temp_bytes, hipStream_t s);
 extern "C" hipError_t lvg_tr_launch(int stage, const void *args_dev, int nb_lines, int nb_lay, int nb_sel, hipStream_t s);
@@ -61,6 +68,7 @@ struct lvg_handle {
     int nb_comp = 0;
     int has_overlap = 0;
     int cus = 0, blocks_per_cu = 1;
+    int big = 0;                   // N > 256: the 768-thread block kernel (lvg_kernels_big.hip)
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     LvgDevProblem P{};
@@ -418,8 +426,8 @@ int validate(lvg_handle *h, const lvg_problem *p) {
     if (!p || !p->mol || !p->coll || !p->esc) return fail(h, LVG_E_ARG, "problem, molecule, collisions and escape table are required");
     const lvg_molecule &M = *p->mol;
     if (M.nb_lev < 2) return fail(h, LVG_E_ARG, "nb_lev must be >= 2");
-    if (M.nb_lev > lvg_kernel_max_levels())
-        return fail(h, LVG_E_UNSUPPORTED, "nb_lev %d exceeds this build's %d", M.nb_lev, lvg_kernel_max_levels());
+    if (M.nb_lev > lvg_kernel_max_levels_big())
+        return fail(h, LVG_E_UNSUPPORTED, "nb_lev %d exceeds this build's %d", M.nb_lev, lvg_kernel_max_levels_big());
     if (!M.energy || !M.g || !M.einst || !(M.mass > 0.)) return fail(h, LVG_E_ARG, "molecule arrays / mass missing");
     if (!ascending(M.energy, M.nb_lev, false)) return fail(h, LVG_E_ARG, "level energies must be ascending");
     for (int i = 0; i < M.nb_lev; i++) if (M.g[i] <= 0) return fail(h, LVG_E_ARG, "g[%d] must be positive", i);
@@ -708,7 +716,8 @@ int lvg_create(const lvg_problem *prob, int device, lvg_handle **out) {
                 hipMemcpy(h->d_prob, &h->P, sizeof(LvgDevProblem), hipMemcpyHostToDevice) != hipSuccess)
                 rc = fail(h, LVG_E_DEVICE, "problem block upload failed");
             int b = 1;
-            if (lvg_kernel_occupancy(&b) != hipSuccess || b < 1) b = 1;
+            h->big = h->N > lvg_kernel_max_levels();
+            if ((h->big ? lvg_kernel_occupancy_big(&b) : lvg_kernel_occupancy(&b)) != hipSuccess || b < 1) b = 1;
             h->blocks_per_cu = b;
         }
     }
@@ -814,7 +823,7 @@ int launch_solve(lvg_handle *h, int nb_lay, const double *d_soa, double *d_pops,
     HIPCHECK(h, hipMemsetAsync(h->counter, 0, sizeof(int), s));
     HIPCHECK(h, hipEventRecord(h->ev0, s));
     if (wave) HIPCHECK(h, lvg_launch_solve_wave(h->d_prob, dL, h->N, grid, wpb, wdyn, s));
-    else HIPCHECK(h, lvg_launch_solve(h->d_prob, dL, grid, s));
+    else HIPCHECK(h, h->big ? lvg_launch_solve_big(h->d_prob, dL, grid, s) : lvg_launch_solve(h->d_prob, dL, grid, s));
     HIPCHECK(h, hipEventRecord(h->ev1, s));
     h->last_launches = 1;
     if (!stream) {
@@ -975,7 +984,7 @@ int lvg_debug_calc_new_pop(lvg_handle *h, const lvg_layers *layers, int layer, c
     if ((rc = push_launch(h, L, 0, h->stream, &dL))) { (void)hipFree(dbg); return rc; }
     hipError_t e = hipMemcpy(L.dbg_pop_in, pop_in, sizeof(double) * N, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-    if (e == hipSuccess) e = lvg_launch_debug(h->d_prob, dL, h->stream);
+    if (e == hipSuccess) e = h->big ? lvg_launch_debug_big(h->d_prob, dL, h->stream) : lvg_launch_debug(h->d_prob, dL, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     std::vector<double> host((size_t)N * N + 3 * N + 1);
     if (e == hipSuccess) e = hipMemcpy(host.data(), dbg, sizeof(double) * host.size(), hipMemcpyDeviceToHost);
@@ -1014,7 +1023,7 @@ int lvg_boundary_layer_populations(lvg_handle *h, const lvg_layers *layers, doub
     const LvgLaunch *dL = nullptr;
     if ((rc = push_launch(h, L, 0, h->stream, &dL))) return rc;
     HIPCHECK(h, hipMemsetAsync(h->counter, 0, sizeof(int), h->stream));
-    HIPCHECK(h, lvg_launch_solve(h->d_prob, dL, grid, h->stream));
+    HIPCHECK(h, h->big ? lvg_launch_solve_big(h->d_prob, dL, grid, h->stream) : lvg_launch_solve(h->d_prob, dL, grid, h->stream));
     HIPCHECK(h, hipStreamSynchronize(h->stream));
     HIPCHECK(h, hipMemcpy(pops_out, h->d_pops, sizeof(double) * (size_t)nl * N, hipMemcpyDeviceToHost));
     return LVG_OK;
@@ -1181,7 +1190,8 @@ int lvg_lim_luminosity(lvg_handle *h, const lvg_layers *layers, const lvg_cloud_
     const LvgLaunch *dL = nullptr;
     if ((rc = push_launch(h, L, 0, h->stream, &dL))) return rc;
     HIPCHECK(h, hipMemsetAsync(h->counter, 0, sizeof(int), h->stream));
-    HIPCHECK(h, lvg_launch_lum(h->d_prob, dL, d_args, grid, nb_trans, nl, h->stream));
+    HIPCHECK(h, h->big ? lvg_launch_lum_big(h->d_prob, dL, d_args, grid, nb_trans, nl, h->stream)
+                       : lvg_launch_lum(h->d_prob, dL, d_args, grid, nb_trans, nl, h->stream));
     HIPCHECK(h, hipStreamSynchronize(h->stream));
     if (lum) HIPCHECK(h, hipMemcpy(lum, d_lum, sizeof(double) * nb_trans, hipMemcpyDeviceToHost));
     double *outs[5] = {lum_arr, emiss_coeff_arr, pump_rate_arr, pump_eff_arr, loss_rate_arr};

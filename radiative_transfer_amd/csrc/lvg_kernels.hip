@@ -26,7 +26,39 @@
 #include "../../include/lvg_amd.h"
 #include "../../include/lvg_math.h"
 
-namespace lvg {
+// Instantiation. The product library compiles this file twice: as is (namespace lvg,
+// 256 threads, N <= 256, 2 workgroups per CU) and through lvg_kernels_big.hip
+// (LVG_BIG: namespace lvg_big, 768 threads, N <= 768 — the reference's CH3OH
+// callers, radiative_transfer.cpp:647, :773 — one workgroup per CU, the whole LDS).
+// The algorithm, the operation order and hence the results are the same; every
+// extern "C" entry of the second copy carries the suffix _big.
+#ifndef LVG_BIG
+#define LVG_BIG 0
+#endif
+#if LVG_BIG
+#define LVG_NS lvg_big
+#define LVG_SYM(name) name##_big
+#ifndef LVG_BT
+#define LVG_BT 768
+#endif
+#ifndef LVG_NMAX
+#define LVG_NMAX 768
+#endif
+#ifndef LVG_OCC
+#define LVG_OCC 1
+#endif
+#else
+#define LVG_NS lvg
+#define LVG_SYM(name) name
+#ifndef LVG_BT
+#define LVG_BT 256
+#endif
+#ifndef LVG_NMAX
+#define LVG_NMAX 256
+#endif
+#endif
+
+namespace LVG_NS {
 
 // Diagnostic build only (-DLVG_PHASE_TIMERS): per-phase s_memtime cycle sums,
 // thread 0 of every block, flushed to lvg_phase_cycles[]. Never in the product .so.
@@ -56,10 +88,11 @@ __shared__ unsigned long long lvg_ph_lds[32];
 #define PH_FLUSH() do {} while (0)
 #endif
 
-constexpr int BT   = 256;   // threads per workgroup
+constexpr int BT   = LVG_BT;     // threads per workgroup (one panel row per thread: N <= BT)
 constexpr int NW   = BT / 64;
-constexpr int NB   = 16;    // LU panel width
-constexpr int NMAX = 256;   // max levels of this kernel
+constexpr int NB   = 16;         // LU panel width
+constexpr int NMAX = LVG_NMAX;   // max levels of this kernel
+static_assert(NMAX <= BT && BT % 64 == 0 && NMAX % 32 == 0, "one row per thread, whole waves");
 constexpr int NHIST = LVG_HIST_SLOTS;
 
 constexpr double BOLTZMANN_CONSTANT    = 1.380649e-16;
@@ -97,13 +130,13 @@ constexpr double MIN_LINE_OPACITY      = 1.e-99;
 #ifndef LVG_OCC
 #define LVG_OCC 2                     // resident workgroups per CU solve_kernel is built for
 #endif
-constexpr int YCAP = (LVG_OCC >= 3) ? 1 : 2048;   // line terms kept in LDS when 2*nb_lines <= YCAP
+constexpr int YCAP = (LVG_OCC >= 3 || LVG_BIG) ? 1 : 2048;   // line terms kept in LDS when 2*nb_lines <= YCAP
 constexpr int TC = 4;                 // columns per thread in the LU register tile (8 rows x TC)
 constexpr int WB = 8 * TC;            // LU block-column width
 
 struct Smem {
     double pold[NMAX], bvec[NMAX];
-#if LVG_OCC >= 3
+#if LVG_OCC >= 3 || LVG_BIG
     union { double pnew[NMAX]; double blog[NMAX]; };   // pnew only ever copies blog
 #else
     double pnew[NMAX], blog[NMAX];
@@ -113,9 +146,9 @@ struct Smem {
     int    tmap[NMAX];          // physical row of each tile row at the current block load
     int    perm[NMAX];          // LU row permutation: logical position -> physical row
     int    pos[NMAX];           // its inverse: physical row -> logical position
-    double red[8];
-    int    ired[8];
-    unsigned long long pkey[8];   // panel: per-wave pivot keys (|v| bits, active flag), double buffered
+    double red[NW];
+    int    ired[2 * NW];
+    unsigned long long pkey[2 * NW];   // panel: per-wave pivot keys (|v| bits, active flag), double buffered
     double cand[2][NW][NB + 1]; // panel: each wave's pivot candidate row and its b, double buffered
     int    candp[2][NW];        // its physical row
     double L11[NB][NB + 1];
@@ -721,8 +754,8 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
                 wmin = (int)~X;
             }
             if ((t & 63) == 0) {
-                sm.pkey[4 * buf + w] = ((unsigned long long)H << 32) | Lw;
-                sm.ired[4 * buf + w] = wmin;
+                sm.pkey[NW * buf + w] = ((unsigned long long)H << 32) | Lw;
+                sm.ired[NW * buf + w] = wmin;
             }
             if (act && lp == wmin) {               // this wave's candidate publishes its row
 #pragma unroll
@@ -736,7 +769,7 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
             unsigned long long ok[NW];
             int oi[NW];
 #pragma unroll
-            for (int i = 0; i < NW; i++) { ok[i] = sm.pkey[4 * buf + i]; oi[i] = sm.ired[4 * buf + i]; }
+            for (int i = 0; i < NW; i++) { ok[i] = sm.pkey[NW * buf + i]; oi[i] = sm.ired[NW * buf + i]; }
             unsigned long long kmax = ok[0];
             int lmin = oi[0], ww = 0;
 #pragma unroll
@@ -1957,7 +1990,7 @@ __global__ void __launch_bounds__(BT, LVG_OCC) solve_kernel(const LvgDevProblem 
 }
 
 // lvg_debug_calc_new_pop: one calc_new_pop for one layer (block 0 only)
-__global__ void __launch_bounds__(BT, 2) debug_kernel(const LvgDevProblem *__restrict__ Pp,
+__global__ void __launch_bounds__(BT, LVG_OCC) debug_kernel(const LvgDevProblem *__restrict__ Pp,
                                                        const LvgLaunch *__restrict__ Lp) {
     __shared__ Smem sm;
     const LvgDevProblem &P = *Pp;
@@ -1990,7 +2023,7 @@ __global__ void __launch_bounds__(BT, 2) debug_kernel(const LvgDevProblem *__res
 // with the first layer's populations, as the reference, or the layer's own), then the
 // neutral collision rates j -> i for every i (coll_rates.cpp:225-240) in level order,
 // read from the neutral-only collision operator K_n (rate j -> i = K_n[i][j]).
-__global__ void __launch_bounds__(BT, 2) lum_kernel(const LvgDevProblem *__restrict__ Pp,
+__global__ void __launch_bounds__(BT, LVG_OCC) lum_kernel(const LvgDevProblem *__restrict__ Pp,
                                                      const LvgLaunch *__restrict__ Lp,
                                                      const LvgLumArgs *__restrict__ Ap) {
     __shared__ Smem sm;
@@ -2065,29 +2098,32 @@ __global__ void __launch_bounds__(64) lum_reduce_kernel(const LvgLumArgs *__rest
     A.lum[tr] = s / A.height;
 }
 
+#if !LVG_BIG
 #include "lvg_wave.h"
+#endif
 
-}  // namespace lvg
+}  // namespace LVG_NS
 
-extern "C" hipError_t lvg_launch_lum(const LvgDevProblem *P, const LvgLaunch *L, const LvgLumArgs *A, int grid,
+extern "C" hipError_t LVG_SYM(lvg_launch_lum)(const LvgDevProblem *P, const LvgLaunch *L, const LvgLumArgs *A, int grid,
                                      int nb_trans, int nb_lay, hipStream_t s) {
-    hipLaunchKernelGGL(lvg::lum_kernel, dim3(grid), dim3(lvg::BT), 0, s, P, L, A);
-    hipLaunchKernelGGL(lvg::lum_reduce_kernel, dim3((nb_trans + 63) / 64), dim3(64), 0, s, A, nb_lay);
+    hipLaunchKernelGGL(LVG_NS::lum_kernel, dim3(grid), dim3(LVG_NS::BT), 0, s, P, L, A);
+    hipLaunchKernelGGL(LVG_NS::lum_reduce_kernel, dim3((nb_trans + 63) / 64), dim3(64), 0, s, A, nb_lay);
     (void)nb_lay;
     return hipGetLastError();
 }
 
 // P and L are DEVICE pointers to the parameter blocks
-extern "C" hipError_t lvg_launch_solve(const LvgDevProblem *P, const LvgLaunch *L, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(lvg::solve_kernel, dim3(grid), dim3(lvg::BT), 0, s, P, L);
+extern "C" hipError_t LVG_SYM(lvg_launch_solve)(const LvgDevProblem *P, const LvgLaunch *L, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(LVG_NS::solve_kernel, dim3(grid), dim3(LVG_NS::BT), 0, s, P, L);
     return hipGetLastError();
 }
 
-extern "C" hipError_t lvg_launch_debug(const LvgDevProblem *P, const LvgLaunch *L, hipStream_t s) {
-    hipLaunchKernelGGL(lvg::debug_kernel, dim3(1), dim3(lvg::BT), 0, s, P, L);
+extern "C" hipError_t LVG_SYM(lvg_launch_debug)(const LvgDevProblem *P, const LvgLaunch *L, hipStream_t s) {
+    hipLaunchKernelGGL(LVG_NS::debug_kernel, dim3(1), dim3(LVG_NS::BT), 0, s, P, L);
     return hipGetLastError();
 }
 
+#if !LVG_BIG
 // ---- wave-per-layer kernel (lvg_wave.h) for N <= 64 ----------------------------------
 // 1 and the waves per block / dynamic LDS bytes if it applies to N levels with
 // nb_y line terms and grid_doubles escape-grid points; 0 if not.
@@ -2124,19 +2160,20 @@ extern "C" hipError_t lvg_launch_solve_wave(const LvgDevProblem *P, const LvgLau
     return hipGetLastError();
 }
 extern "C" size_t lvg_wave_static_lds(void) { return sizeof(lvg::WaveShared); }
+#endif
 
-extern "C" int lvg_kernel_max_levels(void) { return lvg::NMAX; }
-extern "C" int lvg_kernel_block_threads(void) { return lvg::BT; }
-extern "C" hipError_t lvg_kernel_occupancy(int *blocks_per_cu) {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, lvg::solve_kernel, lvg::BT, 0);
+extern "C" int LVG_SYM(lvg_kernel_max_levels)(void) { return LVG_NS::NMAX; }
+extern "C" int LVG_SYM(lvg_kernel_block_threads)(void) { return LVG_NS::BT; }
+extern "C" hipError_t LVG_SYM(lvg_kernel_occupancy)(int *blocks_per_cu) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, LVG_NS::solve_kernel, LVG_NS::BT, 0);
 }
 
 #ifdef LVG_PHASE_TIMERS
-extern "C" int lvg_debug_phase_cycles(unsigned long long *out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lvg::lvg_phase_cycles), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+extern "C" int LVG_SYM(lvg_debug_phase_cycles)(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(LVG_NS::lvg_phase_cycles), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
     if (reset) {
         unsigned long long z[32] = {0};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(lvg::lvg_phase_cycles), z, sizeof z) != hipSuccess) return -1;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(LVG_NS::lvg_phase_cycles), z, sizeof z) != hipSuccess) return -1;
     }
     return 0;
 }

@@ -85,9 +85,9 @@ def test_rejects_malformed_problems(lib):
     P.overlap2 = None
     rc, msg = _create(lib, P)
     assert rc == -1 and "overlap" in msg
-    # more levels than this build's kernel
+    # more levels than this build's largest kernel (768, the reference's CH3OH count)
     P, _, _ = synth.make_problem("ph2o45_1024", nb_lay=1)
-    N = 300
+    N = 769
     P.mol.energy = np.arange(N, dtype=float)
     P.mol.g = np.ones(N, np.int32)
     P.mol.einst = np.zeros((N, N))
