@@ -1,4 +1,7 @@
-# diagnostic library with per-phase s_memtime counters (tools/phase_timers.py)
-cd "$(dirname "$0")/.." && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -DLVG_PHASE_TIMERS $EXTRA \
-  -I include -I radiative_transfer_amd/csrc radiative_transfer_amd/csrc/lvg_abi.cpp radiative_transfer_amd/csrc/lvg_kernels.hip \
-  radiative_transfer_amd/csrc/lvg_transitions.hip radiative_transfer_amd/csrc/lvg_sched.hip -o radiative_transfer_amd/_lib/liblvg_amd_timers.so
+# diagnostic library with per-phase s_memtime counters (tools/phase_timers.py); other
+# objects from the product build (radiative_transfer_amd/_lib/obj)
+cd "$(dirname "$0")/.." && O=radiative_transfer_amd/_lib/obj && \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -DLVG_PHASE_TIMERS $EXTRA \
+  -c radiative_transfer_amd/csrc/lvg_kernels.hip -o $O/timers.o && \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o radiative_transfer_amd/_lib/liblvg_amd_timers.so \
+  $O/timers.o $O/lvg_kernels_big.o $O/lvg_transitions.o $O/lvg_sched.o $O/lvg_abi.o
