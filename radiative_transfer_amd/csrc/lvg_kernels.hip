@@ -173,6 +173,7 @@ struct Smem {
     int8_t tet[LVG_MAX_CLASSES], tgrp[LVG_MAX_CLASSES];
     double dust[LVG_MAX_DUST];
     int    layer, pidx;
+    unsigned pf_dummy[BT];      // destination of the L2-prefetch DMA loads (never read)
 };
 
 // ------------------------------------------------------------------------------
@@ -189,9 +190,14 @@ struct Smem {
 #ifndef LVG_L2_PREFETCH
 #define LVG_L2_PREFETCH 0
 #endif
-__device__ __forceinline__ int l2_token(const void *p) { return *reinterpret_cast<const int *>(p); }
-__device__ __forceinline__ void l2_token_use(int x) { asm volatile("" ::"v"(x)); }
-
+// L2 prefetch of one 128-byte line per lane with no VGPR and no wait: an LDS-DMA dword
+// load (global_load_lds_dword) into a per-wave dummy LDS slot that is never read. The
+// line lands in L2 (and the CU's vector L1) for the ordinary load that needs it later;
+// the kernel drains these loads (s_waitcnt) before it exits.
+__device__ __forceinline__ void l2_prefetch(const void *p, unsigned *dummy) {
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    __builtin_amdgcn_global_load_lds(p, (__attribute__((address_space(3))) void *)(dummy + 64 * w), 4, 0, 0);
+}
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
@@ -1018,8 +1024,6 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
     // next (the next block column of K/li or A, the next chunk of L), so the loads
     // that need them later hit L2 instead of HBM. Each token is consumed (waited on)
     // only when the next prefetch of its kind is issued, long after it has landed.
-    int pf_blk0 = 0, pf_blk1 = 0, pf_blk2 = 0, pf_l = 0;
-    const int prow_t = t < N ? t : 0;
     __syncthreads();
     for (int c0 = 0; c0 < N; c0 += WB) {
         TSTAMP(tp0);
@@ -1034,19 +1038,19 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
         for (int i = 0; i < 8; i++) prow[i] = (8 * rg + i < N) ? sm.perm[8 * rg + i] : 0;
         const int trow = (t < N) ? sm.perm[t] : 0;   // physical row of tile row t (L staging)
         if (LVG_PANEL_ONEWAVE >= 2 && t < N) sm.tmap[t] = trow;
-        if (LVG_L2_PREFETCH) {
-            l2_token_use(pf_blk0); l2_token_use(pf_blk1); l2_token_use(pf_blk2); l2_token_use(pf_l);
-            if (c0 > 0) pf_l = l2_token(A + (int64_t)trow * N);                    // L of chunk 0
-            const int cn = c0 + WB;                                                  // next block column
+        if (LVG_L2_PREFETCH && t < N) {
+            // the next block column's operands, one block column ahead (every physical row
+            // once: perm is a permutation, whatever it becomes by the next block load)
+            const int cn = c0 + WB;
             if (cn < N) {
-                const int64_t o = (int64_t)prow_t * N + cn;
+                const int64_t o = (int64_t)trow * N + cn;
                 if (FUSED) {
-                    pf_blk0 = l2_token(src.K + o);
-                    pf_blk1 = l2_token(src.K + o + 16);
-                    pf_blk2 = l2_token(src.li + o);
+                    l2_prefetch(src.K + o, sm.pf_dummy);
+                    if (cn + 16 < N) l2_prefetch(src.K + o + 16, sm.pf_dummy);
+                    l2_prefetch(src.li + o, sm.pf_dummy);
                 } else {
-                    pf_blk0 = l2_token(A + o);
-                    pf_blk1 = l2_token(A + o + 16);
+                    l2_prefetch(A + o, sm.pf_dummy);
+                    if (cn + 16 < N) l2_prefetch(A + o + 16, sm.pf_dummy);
                 }
             }
         }
@@ -1210,10 +1214,10 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                 } else {
                     fetch_l(kk, lrow, l11v);
                 }
-                if (LVG_L2_PREFETCH && kk + NB < c0) {
-                    l2_token_use(pf_l);
-                    pf_l = l2_token(A + (int64_t)trow * N + kk + NB);                  // L of the next chunk
-                }
+                if (LVG_L2_PREFETCH && kk + NB < c0 && t < N)
+                    l2_prefetch(A + (int64_t)trow * N + kk + NB, sm.pf_dummy);    // L of the next chunk
+                else if (LVG_L2_PREFETCH && kk + NB == c0 && t < N)
+                    l2_prefetch(A + (int64_t)trow * N, sm.pf_dummy);              // chunk 0, next block column
             } else {
                 const bool la = t < N && sm.pos[trow] >= kk + nb;
 #pragma unroll
@@ -1986,6 +1990,7 @@ __global__ void __launch_bounds__(BT, LVG_OCC) solve_kernel(const LvgDevProblem 
             for (int k = lo; k < hi; k++) prev = solve_layer(P, Lc, k, S, sm, k > lo && prev);
         }
     }
+    if (LVG_L2_PREFETCH) __builtin_amdgcn_s_waitcnt(0);   // no LDS-DMA prefetch outlives the workgroup
     PH_FLUSH();
 }
 
@@ -2015,6 +2020,7 @@ __global__ void __launch_bounds__(BT, LVG_OCC) debug_kernel(const LvgDevProblem 
                                    : block_lu_solve(S.A, N, sm.bvec, sm, src, true);
     for (int i = t; i < N; i += BT) { Lc.pops[i] = sm.blog[i]; Lc.dbg_df[i] = S.df[i]; }
     if (t == 0) Lc.dbg_df[N] = eq;
+    if (LVG_L2_PREFETCH) __builtin_amdgcn_s_waitcnt(0);
 }
 
 // lim_luminosity_lvg (maser_luminosity.cpp:7-106): one workgroup per layer (persistent

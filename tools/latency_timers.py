@@ -1,0 +1,29 @@
+"""Diagnostic (timer build): phase cycles of the single slowest layer of a config, solved alone."""
+import ctypes as C, os, sys
+import numpy as np
+sys.path.insert(0, "/root/repo")
+os.environ.setdefault("LVG_LIB_PATH", "/root/repo/radiative_transfer_amd/_lib/liblvg_amd_timers.so")
+from radiative_transfer_amd import abi, synth, native
+
+name = sys.argv[1] if len(sys.argv) > 1 else "ph2o45_1024"
+P, L, o = synth.make_problem(name)
+opts = abi.default_opts(**o)
+s = native.LvgSolver(P)
+lib = native.load()
+buf = (C.c_ulonglong * 32)()
+_, st = s.solve_layers(L, opts)
+k = int(np.argmax(st["iterations"]))
+sub = L.subset(np.array([k]))
+s.solve_layers(sub, opts)
+lib.lvg_debug_phase_cycles(buf, 1)
+_, ss = s.solve_layers(sub, opts)
+ms, _ = s.last_kernel_time()
+lib.lvg_debug_phase_cycles(buf, 1)
+cyc = np.array(buf[:32], dtype=np.float64)
+names = ["setup+coll", "boundary LU", "line terms", "assemble+resid", "LU panel", "LU swap+trsm", "LU gemm",
+         "LU backsub", "ctl"]
+it = int(ss["iterations"][0])
+print(f"{name}: layer {k} alone, {it} iterations, kernel {ms:.3f} ms = {ms * 1e-3 * 2.3e9 / it:.0f} cyc/iteration at 2.3 GHz")
+for i, n in enumerate(names):
+    print(f"  {n:16s} {cyc[i] / it:10.0f} cyc/iteration")
+print(f"  sum of phases    {cyc[:9].sum() / it:10.0f} cyc/iteration; raw slots {buf[:32]}")
