@@ -115,6 +115,9 @@ constexpr double MIN_LINE_OPACITY      = 1.e-99;
 #ifndef LVG_PANEL_PRIO
 #define LVG_PANEL_PRIO 0
 #endif
+#ifndef LVG_L11_DMA
+#define LVG_L11_DMA 0                 // 1: L11 of the next earlier chunk by LDS-DMA one step ahead (measured slower)
+#endif
 #ifndef LVG_L11_ROWS
 #define LVG_L11_ROWS 0
 #endif
@@ -451,6 +454,12 @@ __device__ __forceinline__ void load_rule_table(const LvgDevProblem &P, Smem &sm
 // ascending column sum, row 0 <- 1. Level pairs (f > s) are walked in 16x16 tiles
 // of the lower triangle, one pair per thread: table reads and the K[f][s] writes
 // are 128-byte row segments, every lane is busy.
+#ifndef LVG_CLS_LDS
+#define LVG_CLS_LDS 1                 // pair classes staged in LDS for the collision build
+#endif
+#ifndef LVG_COLL_PU
+#define LVG_COLL_PU 4                 // 16x16 pair tiles per batch of the collision build
+#endif
 __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P, Smem &sm, double *K, double *B,
                                                           bool electrons = true) {
     const int N = P.N, t = threadIdx.x;
@@ -458,9 +467,22 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
     const int nt = (N + 15) >> 4, ntiles = nt * (nt + 1) / 2;
     const int fl = t >> 4, sl = t & 15;
     TSTAMP(tq0);
+    // the pair classes (one byte per level pair) staged in the LU's panel buffer, which is
+    // free between factorizations, when they fit: one wide coalesced copy instead of a
+    // dependent global load in front of every batch's coefficient loads
+    const int M = N * (N - 1) / 2;
+    const bool cls_lds = LVG_CLS_LDS && M <= (int)sizeof(sm.pu);
+    uint8_t *clsl = reinterpret_cast<uint8_t *>(&sm.pu);
+    if (cls_lds) {
+        const int n16 = M >> 4;
+        const uint4 *src4 = reinterpret_cast<const uint4 *>(P.pair_class);
+        for (int e = t; e < n16; e += BT) reinterpret_cast<uint4 *>(clsl)[e] = src4[e];
+        for (int e = (n16 << 4) + t; e < M; e += BT) clsl[e] = P.pair_class[e];
+        __syncthreads();
+    }
     // batches of PU tiles: indices and classes, then every coefficient load, then
     // the arithmetic and the stores (loads never wait behind stores that might alias)
-    constexpr int PU = 4;
+    constexpr int PU = LVG_COLL_PU;
     int F = 0, S = 0;
     for (int q0 = 0; q0 < ntiles; q0 += PU) {
         int pc[PU], fc[PU], sc[PU], cls[PU];
@@ -471,7 +493,7 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
             if (++S > F) { S = 0; F++; }
         }
 #pragma unroll
-        for (int u = 0; u < PU; u++) cls[u] = pc[u] >= 0 ? P.pair_class[pc[u]] : 0;
+        for (int u = 0; u < PU; u++) cls[u] = pc[u] < 0 ? 0 : cls_lds ? clsl[pc[u]] : P.pair_class[pc[u]];
         // level data of the batch, loaded before any store of it
         double ef[PU], es[PU], gf[PU], gs[PU], af[PU];
 #pragma unroll
@@ -1017,6 +1039,23 @@ __device__ __forceinline__ void back_substitute(const double *A, int N, const do
 
 __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Smem &sm, const LuSrc &src, const bool FUSED) {
     const int t = threadIdx.x;
+    // L11 of an earlier chunk (its 16 pivot rows' L part), fetched one step ahead by
+    // LDS-DMA (global_load_lds_dwordx4: no VGPRs) into a double buffer of its own, so
+    // the TRSM no longer waits on a global load issued behind the previous step's U
+    // stores (vmcnt counts loads and stores in order). Rows padded to 18 doubles
+    // (conflict-free row reads); a separate __shared__ object, so the compiler's LDS-DMA
+    // tracking never makes other LDS reads wait for it.
+    __shared__ __attribute__((aligned(16))) double l11s[2][NB][NB + 2];
+    const bool l11_dma = LVG_L11_DMA && !LVG_PREFETCH_L && !LVG_L11_ROWS && (N & 1) == 0;
+    auto l11_issue = [&](int kn) {      // L11 of chunk kn -> l11s[(kn >> 4) & 1]; kn + 16 <= N
+        const int w = __builtin_amdgcn_readfirstlane(t >> 6), e = t;
+        if (w < 3 && e < NB * 9) {
+            const int r = e / 9, c9 = e - 9 * r;
+            const double *g = A + (int64_t)sm.perm[kn + r] * N + kn + 2 * c9;
+            __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)(
+                reinterpret_cast<char *>(&l11s[(kn >> 4) & 1][0][0]) + 1024 * w), 16, 0, 0);
+        }
+    };
     const int rg = t >> 3, cg = t & 7;
     double s_acc = (t == 0) ? 1. : 0.;             // residual row t (FUSED)
     for (int i = t; i < N; i += BT) { sm.perm[i] = i; sm.pos[i] = i; }
@@ -1123,7 +1162,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
         // current chunk's update (their values are final once the earlier blocks are)
         double lnext[NB], l11next = 0.;
         bool have_next = false;
-        auto fetch_l = [&](int k2, double (&lr)[NB], double &l11) {
+        auto fetch_l = [&](int k2, double (&lr)[NB], double &l11, bool want_l11 = true) {
             const int nb2 = min(NB, N - k2);
             // tile row t is logical row t here (earlier pivots were final at the block
             // load), so rows t >= k2 + nb2 are below the chunk (LVG_LA_TILE: no LDS
@@ -1146,7 +1185,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                 for (int m = 0; m < NB; m++) lr[m] = (la && m < nb2) ? src_l[m] : 0.;
             }
             l11 = 0.;
-            if (!LVG_L11_ROWS) {
+            if (!LVG_L11_ROWS && want_l11) {
                 const int r = t / NB, m = t - r * NB;
                 l11 = (t < NB * NB && r < nb2 && m < r) ? A[(int64_t)sm.perm[k2 + r] * N + k2 + m] : 0.;
             }
@@ -1206,13 +1245,18 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             static_assert(NB * NB <= BT, "one L11 entry per thread");
             double l11v = 0., lrow[NB];
             TSTAMP(tp2);
+            // L11 of this chunk came by DMA during the previous step (kk > 0 of an even-N
+            // block column): drain this wave's DMA (and the U stores before it, long done)
+            // before the barrier that publishes it to the other waves
+            const bool l11_in = l11_dma && kk < c0 && kk > 0;
+            if (l11_in) __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
             if (kk < c0) {
                 if (have_next) {
 #pragma unroll
                     for (int m = 0; m < NB; m++) lrow[m] = lnext[m];
                     l11v = l11next;
                 } else {
-                    fetch_l(kk, lrow, l11v);
+                    fetch_l(kk, lrow, l11v, !l11_in);
                 }
                 if (LVG_L2_PREFETCH && kk + NB < c0 && t < N)
                     l2_prefetch(A + (int64_t)trow * N + kk + NB, sm.pf_dummy);    // L of the next chunk
@@ -1244,7 +1288,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
 #pragma unroll
                         for (int m = 0; m < NB; m++) { sm.L11[r][m] = (m < r) ? lrow[m] : 0.; lrow[m] = 0.; }
                     }
-                } else if (t < NB * NB) {
+                } else if (t < NB * NB && !l11_in) {
                     sm.L11[t / NB][t % NB] = l11v;
                 }
             }
@@ -1264,8 +1308,16 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                     x[q] = (r < nb && c < wJ) ? sm.Ub[r][c] : 0.;
                 }
                 double lrw[NB];
+                if (l11_in) {
 #pragma unroll
-                for (int m = 0; m < NB; m++) lrw[m] = sm.L11[r][m];
+                    for (int m = 0; m < NB; m++) lrw[m] = l11s[(kk >> 4) & 1][r][m];
+                } else {
+#pragma unroll
+                    for (int m = 0; m < NB; m++) lrw[m] = sm.L11[r][m];
+                }
+                // the next earlier chunk's L11, one step ahead (the other buffer's last
+                // reader was the previous step's TRSM)
+                if (l11_dma && kk + NB < c0) l11_issue(kk + NB);
                 // x_m from lane m of each 16-lane row: DPP row_share:m (0x150 + m)
 #define LVG_TRSM_STEP(M_)                                                                  \
                 if ((M_) < nb - 1) {                                                       \
