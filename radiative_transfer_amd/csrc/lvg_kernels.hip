@@ -2194,11 +2194,15 @@ extern "C" int lvg_wave_plan(int N, int nb_y, int grid_doubles, size_t lds_cap, 
     return 0;
 }
 
+// instantiations every 8 levels from 24 up (the unrolled row loops run to NM): OH-HF 24
+// and p-H2O 45 run NM = 24 and 48, the reference's OH-HF 56 runs NM = 56
+#define LVG_WAVE_NMS(X) X(16) X(24) X(32) X(40) X(48) X(56) X(64)
+static int wave_nm(int N) { return N <= 16 ? 16 : ((N + 7) / 8) * 8; }
 static const void *wave_kernel(int N) {
-    if (N <= 16) return reinterpret_cast<const void *>(&lvg::solve_wave_kernel<16>);
-    if (N <= 32) return reinterpret_cast<const void *>(&lvg::solve_wave_kernel<32>);
-    if (N <= 48) return reinterpret_cast<const void *>(&lvg::solve_wave_kernel<48>);
-    return reinterpret_cast<const void *>(&lvg::solve_wave_kernel<64>);
+#define LVG_WK(NM_) if (wave_nm(N) == NM_) return reinterpret_cast<const void *>(&lvg::solve_wave_kernel<NM_>);
+    LVG_WAVE_NMS(LVG_WK)
+#undef LVG_WK
+    return nullptr;
 }
 
 extern "C" hipError_t lvg_wave_occupancy(int N, int wpb, size_t dyn, int *blocks_per_cu) {
@@ -2211,10 +2215,9 @@ extern "C" hipError_t lvg_wave_occupancy(int N, int wpb, size_t dyn, int *blocks
 extern "C" hipError_t lvg_launch_solve_wave(const LvgDevProblem *P, const LvgLaunch *L, int N, int grid, int wpb,
                                             size_t dyn, hipStream_t s) {
     const dim3 g(grid), b(64 * wpb);
-    if (N <= 16) hipLaunchKernelGGL(lvg::solve_wave_kernel<16>, g, b, dyn, s, P, L);
-    else if (N <= 32) hipLaunchKernelGGL(lvg::solve_wave_kernel<32>, g, b, dyn, s, P, L);
-    else if (N <= 48) hipLaunchKernelGGL(lvg::solve_wave_kernel<48>, g, b, dyn, s, P, L);
-    else hipLaunchKernelGGL(lvg::solve_wave_kernel<64>, g, b, dyn, s, P, L);
+#define LVG_WL(NM_) if (wave_nm(N) == NM_) hipLaunchKernelGGL(lvg::solve_wave_kernel<NM_>, g, b, dyn, s, P, L);
+    LVG_WAVE_NMS(LVG_WL)
+#undef LVG_WL
     return hipGetLastError();
 }
 extern "C" size_t lvg_wave_static_lds(void) { return sizeof(lvg::WaveShared); }

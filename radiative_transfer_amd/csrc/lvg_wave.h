@@ -39,6 +39,13 @@ struct WaveLayer {                // per-wave LDS
     double dust[LVG_MAX_DUST];
 };
 
+#ifdef LVG_PHASE_TIMERS
+// timer build: every wave's lane 0 accumulates (LDS atomics), not just thread 0 of the block
+#undef TACC
+#define TACC(ph, v0) do { if ((threadIdx.x & 63) == 0) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    atomicAdd(&lvg_ph_lds[ph], t_ - (v0)); } } while (0)
+#endif
+
 struct WaveShared {               // per-block LDS (static part)
     int8_t ttab[LVG_MAX_CLASSES][LVG_MAX_TERMS], tcombo[LVG_MAX_CLASSES][LVG_MAX_TERMS];
     int8_t tet[LVG_MAX_CLASSES], tgrp[LVG_MAX_CLASSES];
@@ -49,9 +56,18 @@ struct WaveShared {               // per-block LDS (static part)
 // dynamic LDS: line index map [N][N|1] (int), then K [wpb][N][N|1] (double)
 extern __shared__ double lvg_wave_dyn[];
 
-// LDS and global stores of one lane become visible to the other lanes of its wave
-// (s_waitcnt 0: the wave's own stores have completed before any lane reads them back)
+// LDS stores of one lane become visible to the other lanes of its wave (workgroup-scope
+// fences: lgkmcnt(0); no wait for outstanding global stores, which a lane only reads
+// back itself, in program order)
 __device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+// ... and global stores too (s_waitcnt 0: the wave's own stores have completed), before a
+// lane reads global data another lane wrote: the Ng history rings (accel_step) and the
+// boundary-layer matrix B
+__device__ __forceinline__ void wave_sync_global() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
@@ -480,6 +496,7 @@ __device__ __forceinline__ void wave_next_step_pre(Ctl &C, Slot &S, int N, WaveL
     if (t < N) ring(S.prev, C.hp, 0, N)[t] = sm.pold[t];
     wave_sync();
     if (C.acceleration && (C.iter_nb == C.accel_start || C.nb_after_accel == C.accel_period)) {
+        wave_sync_global();             // the rings are read across lanes
         wave_accel_step(C, S, N, sm);
         C.nb_after_accel = 0;
     }
@@ -530,7 +547,8 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
     lvg_layer_status *st = reinterpret_cast<lvg_layer_status *>(Lc.status) + l;
     const bool need_boundary = (Lc.init != LVG_INIT_GIVEN);
     wave_collisions(P, sh, sm, K, ldk, (need_boundary && !from_prev) ? S.A : nullptr);
-    wave_sync();
+    if (need_boundary && !from_prev) wave_sync_global();   // B is read across lanes
+    else wave_sync();
     TACC(PH_SETUP, ts0);
     if (!need_boundary) {
         if (t < N) { sm.pold[t] = pops[t]; S.given[t] = pops[t]; }

@@ -7,7 +7,8 @@
   the init modes — on CH3OH-A (N = 256) and on p-H2O forced onto the block kernel.
 - The reference's own level counts and the kernel instantiations they select (item 6,
   ADVICE): N = 12 / 64 (wave kernel NM = 16 / 64), OH-HF N = 56 (radiative_transfer.cpp
-  :419, wave NM = 64), H2O N = 150 (:901), CH3OH N = 160 (block kernel, 129..255 rows).
+  :419, wave NM = 56), H2O N = 150 (:901), CH3OH N = 160 (block kernel, 129..255 rows);
+  N = 33 for the NM = 40 instantiation (OH-HF 24 and p-H2O 45 cover NM = 24 and 48).
 - The OH (non-HF) rule, q10 (coll_rates_oh.cpp:334-347), and the GENERIC base-class
   rule (coll_rates.cpp:181-217, q5 first electron set) (item 8).
 - The three |dx| regions of the overlap scheme (iteration_lvg.cpp:461-500): pure
@@ -60,8 +61,8 @@ def test_block_kernel_option_paths(name, nl, force_block):
     s.close()
 
 
-@pytest.mark.parametrize("name,nlev", [("ph2o45_1024", 12), ("ph2o45_1024", 64), ("oh24_overlap_2048", 56),
-                                       ("ph2o45_1024", 150), ("ch3oha256_4096", 160)])
+@pytest.mark.parametrize("name,nlev", [("ph2o45_1024", 12), ("ph2o45_1024", 33), ("ph2o45_1024", 64),
+                                       ("oh24_overlap_2048", 56), ("ph2o45_1024", 150), ("ch3oha256_4096", 160)])
 def test_reference_level_counts(name, nlev):
     P, L, o = synth.make_problem(name, nb_lay=8, nb_lev=nlev)
     s = LvgSolver(P)
