@@ -25,6 +25,7 @@ constexpr int WNMAX = 64;
 
 struct WaveLayer {                // per-wave LDS
     double pold[WNMAX], pnew[WNMAX], diag[WNMAX];
+    alignas(16) double prow[WNMAX + 2];   // LU: the pivot row of the current column, then its b
     double y[WYCAP];
     double hist_acc[32];
     double T, Te, vw, vgrad, nmol, ne;
@@ -337,8 +338,11 @@ __device__ __forceinline__ void wave_line_terms_overlap(const LvgDevProblem &P, 
 // oracle's (physically swapped) row order, tracked here as each row's logical
 // position lp; every a_ij receives fma(-l_ik, u_kj, a_ij) for k ascending; x_k =
 // b_k / u_kk and b_i = fma(-u_ik, x_k, b_i) for k descending.
+#ifndef LVG_WAVE_LDS_BCAST
+#define LVG_WAVE_LDS_BCAST 0          // 1: pivot row broadcast through LDS (measured slower than v_readlane)
+#endif
 template <int NM>
-__device__ __forceinline__ void wave_lu_solve(double (&a)[NM], double rb, int N, double *x) {
+__device__ __forceinline__ void wave_lu_solve(double (&a)[NM], double rb, int N, double *x, double *pb) {
     const int ln = lane_id();
     TSTAMP(tf0);
     bool act = ln < N;
@@ -366,17 +370,49 @@ __device__ __forceinline__ void wave_lu_solve(double (&a)[NM], double rb, int N,
             }
             pl = __builtin_amdgcn_readfirstlane(pl);
             const int plp = __builtin_amdgcn_readlane(lp, pl);
-            const double piv = readlane_d(a[c], pl);
-            const double bc = readlane_d(rb, pl);
-            if (ln == pl) { act = false; lp = c; }
-            else if (lp == c) lp = plp;
-            const double l = a[c] / piv;
+            double piv, bc;
+            if (LVG_WAVE_LDS_BCAST) {
+                // the pivot lane stores its row from column c (16-byte pairs from c & ~1) and
+                // its b; every lane reads them back (LDS is in order within a wave)
+                const int c2 = c & ~1;
+                if (ln == pl) {
 #pragma unroll
-            for (int j = c + 1; j < NM; j++) {
-                const double u = readlane_d(a[j], pl);
-                if (act) a[j] = fma(-l, u, a[j]);
+                    for (int j = c2; j < NM; j += 2)
+                        *reinterpret_cast<double2 *>(pb + j) = make_double2(a[j], j + 1 < NM ? a[j + 1] : 0.);
+                    pb[NM + (NM & 1)] = rb;
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                double u[NM];
+#pragma unroll
+                for (int j = c2; j < NM; j += 2) {
+                    const double2 v = *reinterpret_cast<const double2 *>(pb + j);
+                    u[j] = v.x;
+                    if (j + 1 < NM) u[j + 1] = v.y;
+                }
+                piv = u[c];
+                bc = pb[NM + (NM & 1)];
+                if (ln == pl) { act = false; lp = c; }
+                else if (lp == c) lp = plp;
+                const double l = a[c] / piv;
+#pragma unroll
+                for (int j = c + 1; j < NM; j++)
+                    if (act) a[j] = fma(-l, u[j], a[j]);
+                if (act) { a[c] = l; rb = fma(-l, bc, rb); }
+                __builtin_amdgcn_wave_barrier();    // reads of pb done before the next column's stores
+            } else {
+                piv = readlane_d(a[c], pl);
+                bc = readlane_d(rb, pl);
+                if (ln == pl) { act = false; lp = c; }
+                else if (lp == c) lp = plp;
+                const double l = a[c] / piv;
+#pragma unroll
+                for (int j = c + 1; j < NM; j++) {
+                    const double u = readlane_d(a[j], pl);
+                    if (act) a[j] = fma(-l, u, a[j]);
+                }
+                if (act) { a[c] = l; rb = fma(-l, bc, rb); }
             }
-            if (act) { a[c] = l; rb = fma(-l, bc, rb); }
         }
     }
     TACC(PH_PANEL, tf0);
@@ -582,18 +618,32 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
             wave_sync();
             TACC(PH_LINES, tl0);
             TSTAMP(ta0);
-            // diagonal (column_diagonals): lane d folds column d of K in the reference order
+            // diagonal (column_diagonals): lane d folds column d of K in the reference order.
+            // Operands come in blocks of 8 (all LDS loads of a block issued before use) and
+            // the data-dependent terms are selects, not branches: same operations, same order.
             double dg = 0.;
             {
                 const int d = row;
                 const bool il = M.diag_interleaved != 0;
 #pragma unroll
-                for (int r = 0; r < NM; r++) {
-                    if (r < N && r != d) {
-                        dg = dg - K[r * ldk + d];
-                        if (il) {
-                            const int lv = li[r * ldk + d];
-                            if (lv >= 0) dg = dg - sm.y[lv];
+                for (int r0 = 0; r0 < NM; r0 += 8) {
+                    double kc[8], yc[8];
+                    int lc[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        const int r = r0 + u;
+                        kc[u] = (r < N) ? K[r * ldk + d] : 0.;
+                        lc[u] = (il && r < N) ? li[r * ldk + d] : -1;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; u++) yc[u] = sm.y[lc[u] >= 0 ? lc[u] : 0];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        const int r = r0 + u;
+                        if (r < N) {
+                            double x = dg - kc[u];
+                            x = (lc[u] >= 0) ? x - yc[u] : x;
+                            dg = (r != d) ? x : dg;
                         }
                     }
                 }
@@ -603,23 +653,37 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
             // row `row` of A = K + line terms, diagonal, row 0 <- 1; residual e0 - A n
             double s = (t == 0) ? 1. : 0.;
 #pragma unroll
-            for (int j = 0; j < NM; j++) {
-                if (j < N) {
-                    double v = K[row * ldk + j];
-                    const int lv = li[row * ldk + j];
-                    if (lv >= 0) v = v + sm.y[lv];
-                    if (j == row) v = dg;
-                    if (row == 0) v = 1.;
-                    a[j] = v;
-                    s = s - v * sm.pold[j];
-                } else {
-                    a[j] = 0.;
+            for (int j0 = 0; j0 < NM; j0 += 8) {
+                double kc[8], yc[8], pc[8];
+                int lc[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int j = j0 + u;
+                    kc[u] = (j < N) ? K[row * ldk + j] : 0.;
+                    lc[u] = (j < N) ? li[row * ldk + j] : -1;
+                    pc[u] = (j < N) ? sm.pold[j] : 0.;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) yc[u] = sm.y[lc[u] >= 0 ? lc[u] : 0];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int j = j0 + u;
+                    if (j < N) {
+                        double v = kc[u];
+                        v = (lc[u] >= 0) ? v + yc[u] : v;
+                        v = (j == row) ? dg : v;
+                        v = (row == 0) ? 1. : v;
+                        a[j] = v;
+                        s = s - v * pc[u];
+                    } else {
+                        a[j] = 0.;
+                    }
                 }
             }
             eq = wave_max(t < N ? fabs(s) : 0.);
             TACC(PH_ASSEMBLE, ta0);
         }
-        wave_lu_solve<NM>(a, t == 0 ? 1. : 0., N, sm.pnew);
+        wave_lu_solve<NM>(a, t == 0 ? 1. : 0., N, sm.pnew, sm.prow);
         wave_sync();
         if (boundary) {
             if (t < N) { sm.pold[t] = sm.pnew[t]; S.given[t] = sm.pnew[t]; }
