@@ -134,7 +134,9 @@ constexpr double MIN_LINE_OPACITY      = 1.e-99;
 #define LVG_OCC 2                     // resident workgroups per CU solve_kernel is built for
 #endif
 constexpr int YCAP = (LVG_OCC >= 3 || LVG_BIG) ? 1 : 2048;   // line terms kept in LDS when 2*nb_lines <= YCAP
-constexpr int TC = 4;                 // columns per thread in the LU register tile (8 rows x TC)
+constexpr int TC = 4;                 // columns per thread in the LU register tile (TR rows x TC)
+constexpr int TR = NMAX * 8 / BT;     // tile rows per thread: the BT/8 row groups cover NMAX
+static_assert(TR * (BT / 8) >= NMAX && TR % 2 == 0, "the register tiles cover every row");
 constexpr int WB = 8 * TC;            // LU block-column width
 
 struct Smem {
@@ -465,7 +467,7 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
     const int N = P.N, t = threadIdx.x;
     const double T = sm.T, Te = sm.Te;
     const int nt = (N + 15) >> 4, ntiles = nt * (nt + 1) / 2;
-    const int fl = t >> 4, sl = t & 15;
+    const int fl = (t >> 4) & 15, sl = t & 15;
     TSTAMP(tq0);
     // the pair classes (one byte per level pair) staged in the LU's panel buffer, which is
     // free between factorizations, when they fit: one wide coalesced copy instead of a
@@ -482,15 +484,20 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
     }
     // batches of PU tiles: indices and classes, then every coefficient load, then
     // the arithmetic and the stores (loads never wait behind stores that might alias)
-    constexpr int PU = LVG_COLL_PU;
-    int F = 0, S = 0;
-    for (int q0 = 0; q0 < ntiles; q0 += PU) {
+    constexpr int PU = LVG_COLL_PU, TG = BT / 256;    // TG groups of 256 threads, PU tiles each
+    const int tg = t >> 8;
+    for (int q0 = 0; q0 < ntiles; q0 += PU * TG) {
         int pc[PU], fc[PU], sc[PU], cls[PU];
 #pragma unroll
         for (int u = 0; u < PU; u++) {
+            // tile q = (F, S), S <= F, in row order of the lower triangle of tiles
+            const int q = q0 + tg * PU + u;
+            int F = (int)((sqrt(8. * q + 1.) - 1.) * 0.5);
+            while (F * (F + 1) / 2 > q) F--;
+            while ((F + 1) * (F + 2) / 2 <= q) F++;
+            const int S = q - F * (F + 1) / 2;
             fc[u] = 16 * F + fl; sc[u] = 16 * S + sl;
-            pc[u] = (q0 + u < ntiles && fc[u] < N && sc[u] < fc[u]) ? fc[u] * (fc[u] - 1) / 2 + sc[u] : -1;
-            if (++S > F) { S = 0; F++; }
+            pc[u] = (q < ntiles && fc[u] < N && sc[u] < fc[u]) ? fc[u] * (fc[u] - 1) / 2 + sc[u] : -1;
         }
 #pragma unroll
         for (int u = 0; u < PU; u++) cls[u] = pc[u] < 0 ? 0 : cls_lds ? clsl[pc[u]] : P.pair_class[pc[u]];
@@ -1056,7 +1063,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                 reinterpret_cast<char *>(&l11s[(kn >> 4) & 1][0][0]) + 1024 * w), 16, 0, 0);
         }
     };
-    const int rg = t >> 3, cg = t & 7;
+    const int rg = t >> 3, cg = t & 7;   // tile rows TR*rg.., columns TC*cg..
     double s_acc = (t == 0) ? 1. : 0.;             // residual row t (FUSED)
     for (int i = t; i < N; i += BT) { sm.perm[i] = i; sm.pos[i] = i; }
     // L2 prefetch tokens: one dword per 128-byte line of the slot's operands read
@@ -1067,14 +1074,14 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
     for (int c0 = 0; c0 < N; c0 += WB) {
         TSTAMP(tp0);
         const int wJ = min(WB, N - c0);
-        double acc[8][TC];
+        double acc[TR][TC];
         // The block column is held in LOGICAL row order as of this load: tile row r is
         // physical row perm[r]. Rows below an earlier block's chunk kk are then the
         // contiguous tile rows >= kk + 16, so whole threads and waves drop out of the
         // updates as kk grows (virtual pivoting alone scatters them).
-        int prow[8];
+        int prow[TR];
 #pragma unroll
-        for (int i = 0; i < 8; i++) prow[i] = (8 * rg + i < N) ? sm.perm[8 * rg + i] : 0;
+        for (int i = 0; i < TR; i++) prow[i] = (TR * rg + i < N) ? sm.perm[TR * rg + i] : 0;
         const int trow = (t < N) ? sm.perm[t] : 0;   // physical row of tile row t (L staging)
         if (LVG_PANEL_ONEWAVE >= 2 && t < N) sm.tmap[t] = trow;
         if (LVG_L2_PREFETCH && t < N) {
@@ -1096,20 +1103,20 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
         // ---- block column c0..c0+wJ-1 into registers (physical rows, coalesced)
         if (!FUSED) {
 #pragma unroll
-            for (int i = 0; i < 8; i++)
+            for (int i = 0; i < TR; i++)
 #pragma unroll
                 for (int j = 0; j < TC; j++) {
                     const int col = TC * cg + j;
-                    acc[i][j] = (8 * rg + i < N && col < wJ) ? A[(int64_t)prow[i] * N + c0 + col] : 0.;
+                    acc[i][j] = (TR * rg + i < N && col < wJ) ? A[(int64_t)prow[i] * N + c0 + col] : 0.;
                 }
         } else {
-            int li[8][TC];
+            int li[TR][TC];
             static_assert(TC == 4, "vector block load assumes 4 columns per thread");
             if ((N & 3) == 0 && TC * cg + TC <= wJ) {
                 // whole 4-column segments, 32-byte aligned: 2 x 16-byte K loads, 1 x 16-byte li load
 #pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    const bool ok = 8 * rg + i < N;
+                for (int i = 0; i < TR; i++) {
+                    const bool ok = TR * rg + i < N;
                     const int64_t o = (int64_t)(ok ? prow[i] : 0) * N + c0 + TC * cg;
                     const double2 k0 = ok ? reinterpret_cast<const double2 *>(src.K + o)[0] : make_double2(0., 0.);
                     const double2 k1 = ok ? reinterpret_cast<const double2 *>(src.K + o)[1] : make_double2(0., 0.);
@@ -1119,18 +1126,18 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                 }
             } else {
 #pragma unroll
-                for (int i = 0; i < 8; i++)
+                for (int i = 0; i < TR; i++)
 #pragma unroll
                     for (int j = 0; j < TC; j++) {
                         const int col = TC * cg + j;
-                        const bool ok = 8 * rg + i < N && col < wJ;
+                        const bool ok = TR * rg + i < N && col < wJ;
                         const int64_t o = (int64_t)prow[i] * N + c0 + col;
                         acc[i][j] = ok ? src.K[o] : 0.;
                         li[i][j] = ok ? src.li[o] : -1;
                     }
             }
 #pragma unroll
-            for (int i = 0; i < 8; i++)
+            for (int i = 0; i < TR; i++)
 #pragma unroll
                 for (int j = 0; j < TC; j++) {
                     const int pr = prow[i], d = c0 + TC * cg + j;
@@ -1139,14 +1146,14 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                     if (pr == d) v = sm.diag[d < NMAX ? d : 0];
                     if (pr == 0) v = 1.;
                     acc[i][j] = v;
-                    if (src.dump && 8 * rg + i < N && TC * cg + j < wJ) src.dump[(int64_t)pr * N + d] = v;
+                    if (src.dump && TR * rg + i < N && TC * cg + j < wJ) src.dump[(int64_t)pr * N + d] = v;
                 }
             // residual rows: 16 columns at a time through LDS, each thread its own row
             for (int h = 0; h < wJ; h += NB) {
                 const int g = cg - h / TC;
                 if (g >= 0 && g < NB / TC) {
 #pragma unroll
-                    for (int i = 0; i < 8; i++)
+                    for (int i = 0; i < TR; i++)
 #pragma unroll
                         for (int j = 0; j < TC; j++) sm.pu.P[prow[i]][TC * g + j] = acc[i][j];
                 }
@@ -1198,8 +1205,8 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                 TSTAMP(tp1);
                 const int g = cg - (kk - c0) / TC;     // this thread's column group within the chunk
 #pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    if (8 * rg + i < N && g >= 0 && g < NB / TC) {
+                for (int i = 0; i < TR; i++) {
+                    if (TR * rg + i < N && g >= 0 && g < NB / TC) {
 #pragma unroll
                         for (int j = 0; j < TC; j++) sm.pu.P[prow[i]][TC * g + j] = acc[i][j];
                     }
@@ -1272,9 +1279,9 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             //      earlier block's chunk they are tile rows kk.. (logical order as of
             //      the block load, when those pivots were already final).
 #pragma unroll
-            for (int i = 0; i < 8; i++) {
-                if (8 * rg + i < N) {
-                    const int q = (kk < c0 ? 8 * rg + i : sm.pos[prow[i]]) - kk;
+            for (int i = 0; i < TR; i++) {
+                if (TR * rg + i < N) {
+                    const int q = (kk < c0 ? TR * rg + i : sm.pos[prow[i]]) - kk;
                     if (q >= 0 && q < nb) {
 #pragma unroll
                         for (int j = 0; j < TC; j++) sm.Ub[q][TC * cg + j] = acc[i][j];
@@ -1343,8 +1350,10 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             TACC(PH_T_SOLVE, tp2s);
             TSTAMP(tp2t);
             // ---- staged L, transposed (thread per row: conflict-free LDS writes)
+            if (t < NMAX) {
 #pragma unroll
-            for (int m = 0; m < NB; m++) sm.pu.LT[m][t] = lrow[m];
+                for (int m = 0; m < NB; m++) sm.pu.LT[m][t] = lrow[m];
+            }
             __syncthreads();
             TACC(PH_T_STAGE, tp2t);
             have_next = LVG_PREFETCH_L && kk + NB < c0;
@@ -1357,33 +1366,33 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             //      so whatever lands in their registers is never read again.
             bool any = false;
             if (kk < c0) {
-                any = 8 * rg + 7 >= kk + nb && 8 * rg < N;   // contiguous suffix of tile rows
+                any = TR * rg + TR - 1 >= kk + nb && TR * rg < N;   // contiguous suffix of tile rows
             } else {
 #pragma unroll
-                for (int i = 0; i < 8; i++) any = any || (8 * rg + i < N && sm.pos[prow[i]] >= kk + nb);
+                for (int i = 0; i < TR; i++) any = any || (TR * rg + i < N && sm.pos[prow[i]] >= kk + nb);
             }
             if (any && TC * cg + TC - 1 >= jlo) {
                 // operands of step m+1 are read from LDS while step m computes
-                double a0[8], u0[TC], a1[8], u1[TC];
-                auto ld = [&](int m, double (&a)[8], double (&u)[TC]) {
+                double a0[TR], u0[TC], a1[TR], u1[TC];
+                auto ld = [&](int m, double (&a)[TR], double (&u)[TC]) {
                     if (LVG_GEMM_B128) {
                         // 16-byte LDS reads (ds_read_b128: half the LDS cycles of ds_read2_b64)
-                        const double2 *ap = reinterpret_cast<const double2 *>(&sm.pu.LT[m][8 * rg]);
+                        const double2 *ap = reinterpret_cast<const double2 *>(&sm.pu.LT[m][TR * rg]);
                         const double2 *up = reinterpret_cast<const double2 *>(&sm.Ub[m][TC * cg]);
 #pragma unroll
-                        for (int i = 0; i < 4; i++) { const double2 v = ap[i]; a[2 * i] = v.x; a[2 * i + 1] = v.y; }
+                        for (int i = 0; i < TR / 2; i++) { const double2 v = ap[i]; a[2 * i] = v.x; a[2 * i + 1] = v.y; }
 #pragma unroll
                         for (int j = 0; j < TC / 2; j++) { const double2 v = up[j]; u[2 * j] = v.x; u[2 * j + 1] = v.y; }
                     } else {
 #pragma unroll
-                        for (int i = 0; i < 8; i++) a[i] = sm.pu.LT[m][8 * rg + i];
+                        for (int i = 0; i < TR; i++) a[i] = sm.pu.LT[m][TR * rg + i];
 #pragma unroll
                         for (int j = 0; j < TC; j++) u[j] = sm.Ub[m][TC * cg + j];
                     }
                 };
-                auto upd = [&](const double (&a)[8], const double (&u)[TC]) {
+                auto upd = [&](const double (&a)[TR], const double (&u)[TC]) {
 #pragma unroll
-                    for (int i = 0; i < 8; i++)
+                    for (int i = 0; i < TR; i++)
 #pragma unroll
                         for (int j = 0; j < TC; j++) acc[i][j] = fma(-a[i], u[j], acc[i][j]);
                 };
