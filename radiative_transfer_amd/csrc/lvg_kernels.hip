@@ -115,9 +115,6 @@ constexpr double MIN_LINE_OPACITY      = 1.e-99;
 #ifndef LVG_PANEL_PRIO
 #define LVG_PANEL_PRIO 0
 #endif
-#ifndef LVG_L11_DMA
-#define LVG_L11_DMA 0                 // 1: L11 of the next earlier chunk by LDS-DMA one step ahead (measured slower)
-#endif
 #ifndef LVG_L11_ROWS
 #define LVG_L11_ROWS 0
 #endif
@@ -126,9 +123,6 @@ constexpr double MIN_LINE_OPACITY      = 1.e-99;
 #endif
 #ifndef LVG_PANEL_ONEWAVE
 #define LVG_PANEL_ONEWAVE 2
-#endif
-#ifndef LVG_LU_MFMA
-#define LVG_LU_MFMA 0                 // 1: rank-16 updates on the matrix cores (block_lu_solve_mfma; 471K vs 511K layer-it/s, kept as a variant)
 #endif
 #ifndef LVG_OCC
 #define LVG_OCC 2                     // resident workgroups per CU solve_kernel is built for
@@ -161,7 +155,6 @@ struct Smem {
     union alignas(16) {
         double P[NMAX][NB + 1]; // panel, physical rows
         double LT[NB][NMAX];    // L of one chunk, transposed, physical rows
-        double Ub1[NB][WB + 2]; // MFMA LU: second U buffer of the earlier-chunk steps
         double hist_acc[32];    // accel_step sums (used outside the LU only)
     } pu;
     // per-layer scalars
@@ -178,7 +171,6 @@ struct Smem {
     int8_t tet[LVG_MAX_CLASSES], tgrp[LVG_MAX_CLASSES];
     double dust[LVG_MAX_DUST];
     int    layer, pidx;
-    unsigned pf_dummy[BT];      // destination of the L2-prefetch DMA loads (never read)
 };
 
 // ------------------------------------------------------------------------------
@@ -192,17 +184,6 @@ struct Smem {
 #ifndef LVG_PANEL_BALLOT
 #define LVG_PANEL_BALLOT 1
 #endif
-#ifndef LVG_L2_PREFETCH
-#define LVG_L2_PREFETCH 0
-#endif
-// L2 prefetch of one 128-byte line per lane with no VGPR and no wait: an LDS-DMA dword
-// load (global_load_lds_dword) into a per-wave dummy LDS slot that is never read. The
-// line lands in L2 (and the CU's vector L1) for the ordinary load that needs it later;
-// the kernel drains these loads (s_waitcnt) before it exits.
-__device__ __forceinline__ void l2_prefetch(const void *p, unsigned *dummy) {
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    __builtin_amdgcn_global_load_lds(p, (__attribute__((address_space(3))) void *)(dummy + 64 * w), 4, 0, 0);
-}
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
@@ -1046,23 +1027,6 @@ __device__ __forceinline__ void back_substitute(const double *A, int N, const do
 
 __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Smem &sm, const LuSrc &src, const bool FUSED) {
     const int t = threadIdx.x;
-    // L11 of an earlier chunk (its 16 pivot rows' L part), fetched one step ahead by
-    // LDS-DMA (global_load_lds_dwordx4: no VGPRs) into a double buffer of its own, so
-    // the TRSM no longer waits on a global load issued behind the previous step's U
-    // stores (vmcnt counts loads and stores in order). Rows padded to 18 doubles
-    // (conflict-free row reads); a separate __shared__ object, so the compiler's LDS-DMA
-    // tracking never makes other LDS reads wait for it.
-    __shared__ __attribute__((aligned(16))) double l11s[2][NB][NB + 2];
-    const bool l11_dma = LVG_L11_DMA && !LVG_PREFETCH_L && !LVG_L11_ROWS && (N & 1) == 0;
-    auto l11_issue = [&](int kn) {      // L11 of chunk kn -> l11s[(kn >> 4) & 1]; kn + 16 <= N
-        const int w = __builtin_amdgcn_readfirstlane(t >> 6), e = t;
-        if (w < 3 && e < NB * 9) {
-            const int r = e / 9, c9 = e - 9 * r;
-            const double *g = A + (int64_t)sm.perm[kn + r] * N + kn + 2 * c9;
-            __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)(
-                reinterpret_cast<char *>(&l11s[(kn >> 4) & 1][0][0]) + 1024 * w), 16, 0, 0);
-        }
-    };
     const int rg = t >> 3, cg = t & 7;   // tile rows TR*rg.., columns TC*cg..
     double s_acc = (t == 0) ? 1. : 0.;             // residual row t (FUSED)
     for (int i = t; i < N; i += BT) { sm.perm[i] = i; sm.pos[i] = i; }
@@ -1084,22 +1048,6 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
         for (int i = 0; i < TR; i++) prow[i] = (TR * rg + i < N) ? sm.perm[TR * rg + i] : 0;
         const int trow = (t < N) ? sm.perm[t] : 0;   // physical row of tile row t (L staging)
         if (LVG_PANEL_ONEWAVE >= 2 && t < N) sm.tmap[t] = trow;
-        if (LVG_L2_PREFETCH && t < N) {
-            // the next block column's operands, one block column ahead (every physical row
-            // once: perm is a permutation, whatever it becomes by the next block load)
-            const int cn = c0 + WB;
-            if (cn < N) {
-                const int64_t o = (int64_t)trow * N + cn;
-                if (FUSED) {
-                    l2_prefetch(src.K + o, sm.pf_dummy);
-                    if (cn + 16 < N) l2_prefetch(src.K + o + 16, sm.pf_dummy);
-                    l2_prefetch(src.li + o, sm.pf_dummy);
-                } else {
-                    l2_prefetch(A + o, sm.pf_dummy);
-                    if (cn + 16 < N) l2_prefetch(A + o + 16, sm.pf_dummy);
-                }
-            }
-        }
         // ---- block column c0..c0+wJ-1 into registers (physical rows, coalesced)
         if (!FUSED) {
 #pragma unroll
@@ -1169,7 +1117,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
         // current chunk's update (their values are final once the earlier blocks are)
         double lnext[NB], l11next = 0.;
         bool have_next = false;
-        auto fetch_l = [&](int k2, double (&lr)[NB], double &l11, bool want_l11 = true) {
+        auto fetch_l = [&](int k2, double (&lr)[NB], double &l11) {
             const int nb2 = min(NB, N - k2);
             // tile row t is logical row t here (earlier pivots were final at the block
             // load), so rows t >= k2 + nb2 are below the chunk (LVG_LA_TILE: no LDS
@@ -1192,7 +1140,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                 for (int m = 0; m < NB; m++) lr[m] = (la && m < nb2) ? src_l[m] : 0.;
             }
             l11 = 0.;
-            if (!LVG_L11_ROWS && want_l11) {
+            if (!LVG_L11_ROWS) {
                 const int r = t / NB, m = t - r * NB;
                 l11 = (t < NB * NB && r < nb2 && m < r) ? A[(int64_t)sm.perm[k2 + r] * N + k2 + m] : 0.;
             }
@@ -1252,23 +1200,14 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             static_assert(NB * NB <= BT, "one L11 entry per thread");
             double l11v = 0., lrow[NB];
             TSTAMP(tp2);
-            // L11 of this chunk came by DMA during the previous step (kk > 0 of an even-N
-            // block column): drain this wave's DMA (and the U stores before it, long done)
-            // before the barrier that publishes it to the other waves
-            const bool l11_in = l11_dma && kk < c0 && kk > 0;
-            if (l11_in) __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
             if (kk < c0) {
                 if (have_next) {
 #pragma unroll
                     for (int m = 0; m < NB; m++) lrow[m] = lnext[m];
                     l11v = l11next;
                 } else {
-                    fetch_l(kk, lrow, l11v, !l11_in);
+                    fetch_l(kk, lrow, l11v);
                 }
-                if (LVG_L2_PREFETCH && kk + NB < c0 && t < N)
-                    l2_prefetch(A + (int64_t)trow * N + kk + NB, sm.pf_dummy);    // L of the next chunk
-                else if (LVG_L2_PREFETCH && kk + NB == c0 && t < N)
-                    l2_prefetch(A + (int64_t)trow * N, sm.pf_dummy);              // chunk 0, next block column
             } else {
                 const bool la = t < N && sm.pos[trow] >= kk + nb;
 #pragma unroll
@@ -1295,7 +1234,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
 #pragma unroll
                         for (int m = 0; m < NB; m++) { sm.L11[r][m] = (m < r) ? lrow[m] : 0.; lrow[m] = 0.; }
                     }
-                } else if (t < NB * NB && !l11_in) {
+                } else if (t < NB * NB) {
                     sm.L11[t / NB][t % NB] = l11v;
                 }
             }
@@ -1315,16 +1254,8 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                     x[q] = (r < nb && c < wJ) ? sm.Ub[r][c] : 0.;
                 }
                 double lrw[NB];
-                if (l11_in) {
 #pragma unroll
-                    for (int m = 0; m < NB; m++) lrw[m] = l11s[(kk >> 4) & 1][r][m];
-                } else {
-#pragma unroll
-                    for (int m = 0; m < NB; m++) lrw[m] = sm.L11[r][m];
-                }
-                // the next earlier chunk's L11, one step ahead (the other buffer's last
-                // reader was the previous step's TRSM)
-                if (l11_dma && kk + NB < c0) l11_issue(kk + NB);
+                for (int m = 0; m < NB; m++) lrw[m] = sm.L11[r][m];
                 // x_m from lane m of each 16-lane row: DPP row_share:m (0x150 + m)
 #define LVG_TRSM_STEP(M_)                                                                  \
                 if ((M_) < nb - 1) {                                                       \
@@ -1420,340 +1351,6 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
     return FUSED ? block_max(emax, sm) : 0.;
 }
 
-
-// ------------------------------------------------------------------------------
-// Left-looking blocked LU with the rank-16 updates on the matrix cores (default).
-//
-// v_mfma_f64_16x16x4_f64 computes D = C + sum_k A[.][k] B[k][.] as a chain of fp64
-// fmas in k order (probed bit for bit: tools/probe/mfma_f64_probe.hip), so the
-// per-element update sequence fma(-l_ik, u_kj, a_ij), k ascending, of the unblocked
-// oracle LU is preserved exactly. The MFMA runs on the matrix pipe, beside the VALU
-// work (panel, TRSM, assembly) of this and the co-resident workgroup.
-//
-// Layout: the 32-column block column is held as 16x16 tiles in MFMA accumulators,
-// transposed (M = columns, N = rows), with the M index m standing for column
-// 4(m&3) + (m>>2): lane l of tile (rt, ct) holds row 16rt + (l&15) and the four
-// consecutive columns 16ct + 4(l>>4) + r, r = 0..3 (32-byte vector loads and stores).
-// Row tiles belong to waves round-robin
-// (wave w: rt = w, w+4, w+8, w+12), so each wave's rows, and the L values that
-// update them, are private to it: L goes global -> registers as MFMA B operands
-// (no LDS staging). Rows are in logical order as of the block load (tile row =
-// perm at the load), so for an earlier chunk kk the pivot rows are exactly row tile
-// kk/16 and the rows below are the tiles after it. Per earlier chunk: the owner wave
-// of tile kk/16 solves its pivot rows against L11 in registers (DPP row_newbcast:
-// the 16 rows of a column are one 16-lane DPP row), publishes U in LDS (double
-// buffered) and to A; one barrier; every wave updates its tiles below.
-// ------------------------------------------------------------------------------
-typedef double v4d __attribute__((ext_vector_type(4)));
-
-// workgroup barrier that orders LDS only: outstanding global loads stay in flight
-// (__syncthreads()' fence would wait for them: vmcnt(0)); global stores made before it
-// are read only after a later __syncthreads().
-__device__ __forceinline__ void lds_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-}
-
-__device__ __forceinline__ v4d mfma_f64(double a, double b, v4d c) {
-    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-}
-
-// forward substitution of one column set against L11 (lane row = l & 15): x_m -= L11[m][j] x_j,
-// j ascending (oracle order); x_j broadcast from lane j of the lane's 16-lane row.
-template <int NV>
-__device__ __forceinline__ void trsm16(double (&x)[NV], const double (&lrw)[NB], int nb, int ln) {
-#define LVG_T16_STEP(M_)                                                                   \
-    if ((M_) < nb - 1) {                                                                   \
-        _Pragma("unroll") for (int q = 0; q < NV; q++) {                                   \
-            const double y = dpp_d<0x150 + (M_), 0xf, 0xf>(x[q]);                          \
-            if (ln > (M_)) x[q] = fma(-lrw[M_], y, x[q]);                                  \
-        }                                                                                  \
-    }
-    LVG_T16_STEP(0) LVG_T16_STEP(1) LVG_T16_STEP(2) LVG_T16_STEP(3)
-    LVG_T16_STEP(4) LVG_T16_STEP(5) LVG_T16_STEP(6) LVG_T16_STEP(7)
-    LVG_T16_STEP(8) LVG_T16_STEP(9) LVG_T16_STEP(10) LVG_T16_STEP(11)
-    LVG_T16_STEP(12) LVG_T16_STEP(13) LVG_T16_STEP(14)
-#undef LVG_T16_STEP
-}
-
-__device__ __forceinline__ double block_lu_solve_mfma(double *A, int N, double *b, Smem &sm, const LuSrc &src,
-                                                      const bool FUSED) {
-    const int t = threadIdx.x, l = t & 63, ln = l & 15, lg = l >> 4;
-    const int w = __builtin_amdgcn_readfirstlane(t >> 6);   // wave-uniform: scalar branches on tiles
-    const int ntl = (N + 15) >> 4;                 // row tiles
-    const int cs = 4 * (ln & 3) + (ln >> 2);       // column of MFMA M index ln within a tile
-    double s_acc = (t == 0) ? 1. : 0.;             // residual row t (FUSED)
-    for (int i = t; i < N; i += BT) { sm.perm[i] = i; sm.pos[i] = i; }
-    __syncthreads();
-    for (int c0 = 0; c0 < N; c0 += WB) {
-        TSTAMP(tp0);
-        const int wJ = min(WB, N - c0);
-        if (t < N) sm.tmap[t] = sm.perm[t];
-        __syncthreads();
-        int prow[4];                               // physical row of this lane in each own tile (-1: none)
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int row = 16 * (w + 4 * i) + ln;
-            prow[i] = row < N ? sm.tmap[row] : -1;
-        }
-        // ---- block column c0..c0+wJ-1 into the accumulators (fused assembly)
-        v4d acc[4][2];
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-            for (int ct = 0; ct < 2; ct++) {
-                const int col = 16 * ct + 4 * lg, pr = prow[i], d0 = c0 + col;
-                const bool ok = pr >= 0 && col < wJ;
-                const int64_t o = (int64_t)(ok ? pr : 0) * N + d0;
-                double v[4] = {0., 0., 0., 0.};
-                int li[4] = {-1, -1, -1, -1};
-                if ((N & 3) == 0 && col + 4 <= wJ) {   // 32-byte aligned segment
-                    const double *sp = FUSED ? src.K : A;
-                    const double2 v0 = ok ? reinterpret_cast<const double2 *>(sp + o)[0] : make_double2(0., 0.);
-                    const double2 v1 = ok ? reinterpret_cast<const double2 *>(sp + o)[1] : make_double2(0., 0.);
-                    v[0] = v0.x; v[1] = v0.y; v[2] = v1.x; v[3] = v1.y;
-                    if (FUSED) {
-                        const int4 l4 = ok ? *reinterpret_cast<const int4 *>(src.li + o) : make_int4(-1, -1, -1, -1);
-                        li[0] = l4.x; li[1] = l4.y; li[2] = l4.z; li[3] = l4.w;
-                    }
-                } else {
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        const bool okr = ok && col + r < wJ;
-                        v[r] = okr ? (FUSED ? src.K[o + r] : A[o + r]) : 0.;
-                        if (FUSED) li[r] = okr ? src.li[o + r] : -1;
-                    }
-                }
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    double x = v[r];
-                    const int d = d0 + r;
-                    if (FUSED && ok && col + r < wJ) {
-                        if (li[r] >= 0) x = x + src.y[li[r]];
-                        if (pr == d) x = sm.diag[d];
-                        if (pr == 0) x = 1.;
-                        if (src.dump) src.dump[o + r] = x;
-                    }
-                    acc[i][ct][r] = x;
-                }
-            }
-        if (FUSED) {
-            // residual rows: 16 columns at a time through LDS, each thread its own row
-            for (int h = 0; h < wJ; h += NB) {
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-#pragma unroll
-                    for (int r = 0; r < 4; r++)
-                        if (prow[i] >= 0) sm.pu.P[prow[i]][4 * lg + r] = (h == 0) ? acc[i][0][r] : acc[i][1][r];
-                __syncthreads();
-                const int nc = min(NB, wJ - h);
-                if (t < N)
-                    for (int c = 0; c < nc; c++) s_acc = s_acc - sm.pu.P[t][c] * src.pop[c0 + h + c];
-                __syncthreads();
-            }
-        }
-        TACC(PH_BLOAD, tp0);
-        for (int kk = 0; kk < c0 + wJ; kk += NB) {
-            const int nb = min(NB, N - kk);
-            if (kk < c0) {
-                // ---- earlier chunks kk = 0, 16, .., c0 - 16 (all of them in this inner loop):
-                //      pivot rows = row tile R (owner wave R & 3), rows below = tiles > R.
-                //      The next chunk's L11 (one entry per thread, to LDS) and L operands are
-                //      loaded during the current step.
-                // B operands L[row][k2 + 4g + lg] of this wave's tiles for chunk k2, loaded raw and
-                // unconditionally (no VALU op on the register and no branch around the load, so the
-                // compiler's vmcnt counting keeps them in flight until the MFMA that uses them; the
-                // sign goes on the U operand). Rows past N read row 0 and tiles above the chunk get
-                // values that are never used: neither is ever stored.
-                int prc[4];
-#pragma unroll
-                for (int i = 0; i < 4; i++) prc[i] = prow[i] >= 0 ? prow[i] : 0;
-                auto load_lf = [&](int k2, double (&lf)[4][4]) {
-#pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        const double *src_l = A + (int64_t)prc[i] * N + k2 + lg;
-#pragma unroll
-                        for (int g = 0; g < 4; g++) lf[i][g] = src_l[4 * g];
-                    }
-                };
-                // L11 rows of the next chunk this wave owns (row ln of chunk kr, final): loaded
-                // right after the wave's previous TRSM, four steps before they are used
-                auto load_l11 = [&](int kr, double (&lr)[NB]) {
-                    const double *sp = A + (int64_t)sm.tmap[kr + ln] * N + kr;
-                    if ((N & 1) == 0) {
-#pragma unroll
-                        for (int j = 0; j < NB / 2; j++) {
-                            const double2 v = reinterpret_cast<const double2 *>(sp)[j];
-                            lr[2 * j] = v.x; lr[2 * j + 1] = v.y;
-                        }
-                    } else {
-#pragma unroll
-                        for (int j = 0; j < NB; j++) lr[j] = sp[j];
-                    }
-                };
-                const int klast = c0 - NB;
-                double lf[4][4], lrn[NB];
-                if (NB * w < c0) load_l11(NB * w, lrn);
-                load_lf(0, lf);
-                // TRSM of chunk k3 by its owner on its pivot tile (held in acc[i3]) -> Ub buffer, A
-                auto owner_trsm = [&](int k3, double (*Uo)[WB + 2]) {
-                    const int i3 = (k3 >> 4) >> 2;
-                    double x[8];
-#pragma unroll
-                    for (int i = 0; i < 4; i++)
-                        if (i == i3) {
-#pragma unroll
-                            for (int r = 0; r < 4; r++) { x[r] = acc[i][0][r]; x[4 + r] = acc[i][1][r]; }
-                        }
-                    TSTAMP(tp2s);
-                    trsm16<8>(x, lrn, NB, ln);
-                    const int64_t urow = (int64_t)sm.tmap[k3 + ln] * N + c0;
-#pragma unroll
-                    for (int q = 0; q < 8; q++) {
-                        const int col = 16 * (q >> 2) + 4 * lg + (q & 3);
-                        if (col < wJ) { Uo[ln][col] = x[q]; A[urow + col] = x[q]; }
-                    }
-                    if (k3 + 4 * NB < c0) load_l11(k3 + 4 * NB, lrn);   // this wave's next chunk
-                    TACC(PH_T_SOLVE, tp2s);
-                };
-                if (w == 0) owner_trsm(0, sm.Ub);  // chunk 0: its pivot rows need no update
-                lds_barrier();
-                // Step kk applies U(kk) to the tiles below row tile R. The owner of chunk kk + 16
-                // first updates only its pivot tile, solves it (U(kk+16) into the other buffer)
-                // and issues its remaining MFMAs after the barrier; the other waves issue all of
-                // theirs before it. So the pivot chain per step is 8 MFMAs + one TRSM.
-                for (; kk < c0; kk += NB) {
-                    TSTAMP(tp3);
-                    const int R = kk >> 4, R2 = R + 1;
-                    double (*U)[WB + 2] = (R & 1) ? sm.pu.Ub1 : sm.Ub;
-                    double (*Un)[WB + 2] = (R & 1) ? sm.Ub : sm.pu.Ub1;
-                    const int k2 = min(kk + NB, klast);
-                    double u0[4], u1[4];
-#pragma unroll
-                    for (int g = 0; g < 4; g++) { u0[g] = -U[4 * g + lg][cs]; u1[g] = -U[4 * g + lg][16 + cs]; }
-                    const bool nown = kk + NB < c0 && w == (R2 & 3);
-                    const int iP = nown ? (R2 >> 2) : -1;
-                    auto upd_tile = [&](int i) {
-#pragma unroll
-                        for (int g = 0; g < 4; g++) {
-                            acc[i][0] = mfma_f64(u0[g], lf[i][g], acc[i][0]);
-                            if (wJ > 16) acc[i][1] = mfma_f64(u1[g], lf[i][g], acc[i][1]);
-                        }
-                    };
-                    auto upd_rest = [&]() {
-#pragma unroll
-                        for (int g = 0; g < 4; g++) {
-#pragma unroll
-                            for (int i = 0; i < 4; i++) {
-                                if ((w + 4 * i) > R && (w + 4 * i) < ntl && i != iP) {
-                                    acc[i][0] = mfma_f64(u0[g], lf[i][g], acc[i][0]);
-                                    if (wJ > 16) acc[i][1] = mfma_f64(u1[g], lf[i][g], acc[i][1]);
-                                }
-                                lf[i][g] = A[(int64_t)prc[i] * N + k2 + 4 * g + lg];
-                            }
-                        }
-                    };
-                    if (nown) {
-#pragma unroll
-                        for (int i = 0; i < 4; i++)
-                            if (i == iP) upd_tile(i);
-                        owner_trsm(kk + NB, Un);
-                    }
-                    upd_rest();
-                    lds_barrier();                 // LDS only: the next chunk's L loads stay in flight
-                    TACC(PH_GEMM, tp3);
-                }
-                kk -= NB;                          // the outer loop steps to c0
-            } else {
-                // ---- a chunk of this block column: all updates from k < kk are in; factor it
-                TSTAMP(tp1);
-                const int ch = (kk - c0) >> 4;
-                if (ch == 0 && c0 > 0) __syncthreads();   // the last earlier step's U (pu.Ub1) vs P
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-#pragma unroll
-                    for (int r = 0; r < 4; r++)
-                        if (prow[i] >= 0) sm.pu.P[prow[i]][4 * lg + r] = ch ? acc[i][1][r] : acc[i][0][r];
-                __syncthreads();
-                const int trow = (t < N) ? sm.tmap[t] : 0;
-                if (LVG_PANEL_ONEWAVE >= 2 && (c0 >> 6) != ((N - 1) >> 6) && (c0 >> 7) == ((N - 1) >> 7)) {
-                    const int base = (c0 >> 7) << 7, lw = t & 63;
-                    const int r2[2] = {base + lw < N ? sm.tmap[base + lw] : -1, base + 64 + lw < N ? sm.tmap[base + 64 + lw] : -1};
-                    panel_factor_wave<2>(A, N, kk, nb, b, sm, base >> 6, r2);
-                } else if (LVG_PANEL_ONEWAVE && (c0 >> 6) == ((N - 1) >> 6)) {
-                    const int r1[1] = {t < N ? trow : -1};
-                    panel_factor_wave<1>(A, N, kk, nb, b, sm, c0 >> 6, r1);
-                } else {
-                    panel_factor(A, N, kk, nb, b, sm);
-                }
-                for (int e = t; e < NB * NB; e += BT) {
-                    const int r = e / NB, m = e - r * NB;
-                    sm.L11[r][m] = (r < nb && m < r) ? sm.pu.P[sm.perm[kk + r]][m] : 0.;
-                }
-                __syncthreads();
-                TACC(PH_PANEL, tp1);
-                if (kk - c0 + nb >= wJ) break;     // last chunk of the block column
-                TSTAMP(tq);
-                // pivot rows of this chunk (logical kk.., scattered over the tiles) in columns 16..31
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    if (prow[i] >= 0) {
-                        const int q = sm.pos[prow[i]] - kk;
-                        if (q >= 0 && q < nb) {
-#pragma unroll
-                            for (int r = 0; r < 4; r++) {
-                                const int col = 16 + 4 * lg + r;
-                                if (col < wJ) sm.Ub[q][col] = acc[i][1][r];
-                            }
-                        }
-                    }
-                }
-                __syncthreads();
-                if (w == 0) {
-                    double x[4], lrw[NB];
-#pragma unroll
-                    for (int r = 0; r < 4; r++) x[r] = (ln < nb && 16 + 4 * lg + r < wJ) ? sm.Ub[ln][16 + 4 * lg + r] : 0.;
-#pragma unroll
-                    for (int j = 0; j < NB; j++) lrw[j] = sm.L11[ln][j];
-                    trsm16<4>(x, lrw, nb, ln);
-                    if (ln < nb) {
-                        const int64_t urow = (int64_t)sm.perm[kk + ln] * N + c0;
-#pragma unroll
-                        for (int r = 0; r < 4; r++) {
-                            const int col = 16 + 4 * lg + r;
-                            if (col < wJ) { sm.Ub[ln][col] = x[r]; A[urow + col] = x[r]; }
-                        }
-                    }
-                }
-                __syncthreads();
-                TACC(PH_TRSM, tq);
-                TSTAMP(tu);
-                // rows below the chunk: columns 16..31 -= L (from the panel, in P) U
-                double lf[4][4];
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const bool act = prow[i] >= 0 && sm.pos[prow[i]] >= kk + nb;
-#pragma unroll
-                    for (int g = 0; g < 4; g++) lf[i][g] = act ? -sm.pu.P[prow[i]][4 * g + lg] : 0.;
-                }
-#pragma unroll
-                for (int g = 0; g < 4; g++) {
-                    const double u1 = sm.Ub[4 * g + lg][16 + cs];
-#pragma unroll
-                    for (int i = 0; i < 4; i++)
-                        if ((w + 4 * i) < ntl) acc[i][1] = mfma_f64(u1, lf[i][g], acc[i][1]);
-                }
-                __syncthreads();                   // P is rewritten by the next chunk
-                TACC(PH_GEMM, tu);
-            }
-        }
-    }
-    back_substitute(A, N, b, sm);
-    double emax = 0.;
-    if (FUSED && t < N) { src.df[t] = s_acc; emax = fabs(s_acc); }
-    return FUSED ? block_max(emax, sm) : 0.;
-}
 
 // ------------------------------------------------------------------------------
 // iteration_control (iteration_control.h:84-242)
@@ -1976,8 +1573,7 @@ __device__ __forceinline__ bool solve_layer(const LvgDevProblem &P, const LvgLau
         }
         for (int i = t; i < N; i += BT) sm.bvec[i] = (i == 0) ? 1. : 0.;
         __syncthreads();
-        const double eq = LVG_LU_MFMA ? block_lu_solve_mfma(S.A, N, sm.bvec, sm, src, !boundary)
-                                       : block_lu_solve(S.A, N, sm.bvec, sm, src, !boundary);
+        const double eq = block_lu_solve(S.A, N, sm.bvec, sm, src, !boundary);
         if (boundary) {
             TACC(PH_BOUNDARY, tb0);
             for (int i = t; i < N; i += BT) { sm.pold[i] = sm.blog[i]; S.given[i] = sm.blog[i]; }
@@ -2051,7 +1647,6 @@ __global__ void __launch_bounds__(BT, LVG_OCC) solve_kernel(const LvgDevProblem 
             for (int k = lo; k < hi; k++) prev = solve_layer(P, Lc, k, S, sm, k > lo && prev);
         }
     }
-    if (LVG_L2_PREFETCH) __builtin_amdgcn_s_waitcnt(0);   // no LDS-DMA prefetch outlives the workgroup
     PH_FLUSH();
 }
 
@@ -2077,11 +1672,9 @@ __global__ void __launch_bounds__(BT, LVG_OCC) debug_kernel(const LvgDevProblem 
     __syncthreads();
     LuSrc src;
     src.K = S.K; src.y = yp; src.li = M.line_idx; src.pop = sm.pold; src.df = S.df; src.dump = Lc.dbg_matrix;
-    const double eq = LVG_LU_MFMA ? block_lu_solve_mfma(S.A, N, sm.bvec, sm, src, true)
-                                   : block_lu_solve(S.A, N, sm.bvec, sm, src, true);
+    const double eq = block_lu_solve(S.A, N, sm.bvec, sm, src, true);
     for (int i = t; i < N; i += BT) { Lc.pops[i] = sm.blog[i]; Lc.dbg_df[i] = S.df[i]; }
     if (t == 0) Lc.dbg_df[N] = eq;
-    if (LVG_L2_PREFETCH) __builtin_amdgcn_s_waitcnt(0);
 }
 
 // lim_luminosity_lvg (maser_luminosity.cpp:7-106): one workgroup per layer (persistent
