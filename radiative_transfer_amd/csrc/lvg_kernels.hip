@@ -115,6 +115,9 @@ constexpr double MIN_LINE_OPACITY      = 1.e-99;
 #ifndef LVG_PANEL_PRIO
 #define LVG_PANEL_PRIO 0
 #endif
+#ifndef LVG_UB2
+#define LVG_UB2 1                     // Ub double-buffered by chunk parity: 2 barriers per earlier-chunk step, not 3
+#endif
 #ifndef LVG_L11_ROWS
 #define LVG_L11_ROWS 0
 #endif
@@ -151,7 +154,7 @@ struct Smem {
     double cand[2][NW][NB + 1]; // panel: each wave's pivot candidate row and its b, double buffered
     int    candp[2][NW];        // its physical row
     double L11[NB][NB + 1];
-    alignas(16) double Ub[NB][WB + 2];   // U rows of one chunk across the block column
+    alignas(16) double Ub[2][NB][WB + 2];   // U rows of one chunk across the block column (by chunk parity)
     union alignas(16) {
         double P[NMAX][NB + 1]; // panel, physical rows
         double LT[NB][NMAX];    // L of one chunk, transposed, physical rows
@@ -1147,6 +1150,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
         };
         for (int kk = 0; kk < c0 + wJ; kk += NB) {
             const int nb = min(NB, N - kk);
+            const int ub = LVG_UB2 ? (kk >> 4) & 1 : 0;   // Ub buffer of this chunk
             int jlo;                                   // first block-local column to update
             if (kk >= c0) {
                 // ---- a chunk of this block column: all updates from k < kk are in; factor it
@@ -1223,7 +1227,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                     const int q = (kk < c0 ? TR * rg + i : sm.pos[prow[i]]) - kk;
                     if (q >= 0 && q < nb) {
 #pragma unroll
-                        for (int j = 0; j < TC; j++) sm.Ub[q][TC * cg + j] = acc[i][j];
+                        for (int j = 0; j < TC; j++) sm.Ub[ub][q][TC * cg + j] = acc[i][j];
                     }
                 }
             }
@@ -1251,7 +1255,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
 #pragma unroll
                 for (int q = 0; q < TC / 2; q++) {
                     const int c = (WB / 4) * w + (l >> 4) + 4 * q;
-                    x[q] = (r < nb && c < wJ) ? sm.Ub[r][c] : 0.;
+                    x[q] = (r < nb && c < wJ) ? sm.Ub[ub][r][c] : 0.;
                 }
                 double lrw[NB];
 #pragma unroll
@@ -1274,7 +1278,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
 #pragma unroll
                     for (int q = 0; q < TC / 2; q++) {
                         const int c = (WB / 4) * w + (l >> 4) + 4 * q;
-                        if (c >= jlo && c < wJ) { sm.Ub[r][c] = x[q]; A[prow + c] = x[q]; }
+                        if (c >= jlo && c < wJ) { sm.Ub[ub][r][c] = x[q]; A[prow + c] = x[q]; }
                     }
                 }
             }
@@ -1309,7 +1313,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                     if (LVG_GEMM_B128) {
                         // 16-byte LDS reads (ds_read_b128: half the LDS cycles of ds_read2_b64)
                         const double2 *ap = reinterpret_cast<const double2 *>(&sm.pu.LT[m][TR * rg]);
-                        const double2 *up = reinterpret_cast<const double2 *>(&sm.Ub[m][TC * cg]);
+                        const double2 *up = reinterpret_cast<const double2 *>(&sm.Ub[ub][m][TC * cg]);
 #pragma unroll
                         for (int i = 0; i < TR / 2; i++) { const double2 v = ap[i]; a[2 * i] = v.x; a[2 * i + 1] = v.y; }
 #pragma unroll
@@ -1318,7 +1322,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
 #pragma unroll
                         for (int i = 0; i < TR; i++) a[i] = sm.pu.LT[m][TR * rg + i];
 #pragma unroll
-                        for (int j = 0; j < TC; j++) u[j] = sm.Ub[m][TC * cg + j];
+                        for (int j = 0; j < TC; j++) u[j] = sm.Ub[ub][m][TC * cg + j];
                     }
                 };
                 auto upd = [&](const double (&a)[TR], const double (&u)[TC]) {
@@ -1341,7 +1345,10 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                     for (int m = 0; m < nb; m++) { ld(m, a0, u0); upd(a0, u0); }
                 }
             }
-            __syncthreads();
+            // between two earlier chunks the next step's opening barrier suffices: its Ub goes
+            // to the other buffer, L11 and LT are only rewritten after every wave has left
+            // this step's TRSM / passed that barrier
+            if (!(LVG_UB2 && kk + NB < c0)) __syncthreads();
             TACC(PH_GEMM, tp3);
         }
     }
