@@ -177,7 +177,13 @@ def main():
     opts = abi.default_opts(**o)
     if args.chain_len:
         opts.init = abi.LVG_INIT_WARM_CHAIN
-    lo, hi = dist.shard_range(total, world, rank)
+    if args.chain_len:
+        # clouds of chain_len consecutive layers; whole clouds per rank (dist.chain_shard)
+        offs_all = chain_offsets(total, args.chain_len)
+        c_lo, c_hi = dist.chain_shard(offs_all, world, rank)
+        lo, hi = int(offs_all[c_lo]), int(offs_all[c_hi])
+    else:
+        lo, hi = dist.shard_range(total, world, rank)
     mine = layers_all.subset(np.arange(lo, hi))
     n_mine = hi - lo
 
@@ -187,7 +193,7 @@ def main():
     status = torch.zeros((max(n_mine, 1), abi.STATUS_DTYPE.itemsize // 8), dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev)
 
-    offs = chain_offsets(n_mine, args.chain_len) if args.chain_len else None
+    offs = (offs_all[c_lo:c_hi + 1] - lo).astype(np.int32) if args.chain_len else None
 
     def step():
         if offs is not None:
@@ -265,7 +271,9 @@ def main():
             "config": {"workload": args.workload, "nb_lev": N, "layers_total": total,
                        "layers_per_gpu": hi - lo if world == 1 else f"{total // world}-{-(-total // world)}",
                        "layer_iterations_per_step": units_total, "nonconverged_layers": nonconv,
-                       "max_rel_error": max_rel, "parallelism": f"layers sharded x{world} (dist.shard_range)",
+                       "max_rel_error": max_rel,
+                       "parallelism": f"clouds sharded x{world} (dist.chain_shard)" if args.chain_len
+                       else f"layers sharded x{world} (dist.shard_range)",
                        "init": f"warm_chain x{len(offs) - 1} clouds of {args.chain_len} layers" if offs is not None
                        else "boundary_layer", "acceleration": bool(opts.acceleration),
                        "line_overlap": bool(opts.line_overlap)},

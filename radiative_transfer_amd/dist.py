@@ -6,6 +6,8 @@ blocks, one per rank (one process per GPU). There is no data-path collective:
 the only exchange is the per-solve status reduction below (total
 layer-iterations, non-converged layers, max rel_error), plus an optional
 all_gather of the populations when the caller wants them on every rank.
+Warm chains (the reference's default start rule) are sequential within a cloud, so
+there whole clouds go to ranks (`chain_shard`), contiguous and balanced by layer count.
 The backend is whatever torch.distributed was initialised with: "nccl" (RCCL
 over xGMI) on MI355X nodes, "gloo" in the CPU tests. Collective tensors live on
 the current GPU under nccl (RCCL takes device tensors only) and on the CPU
@@ -32,6 +34,37 @@ def shard_range(n_total: int, world: int, rank: int) -> Tuple[int, int]:
     lo = (n_total * rank) // world
     hi = (n_total * (rank + 1)) // world
     return lo, hi
+
+
+def chain_shard(chain_off, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous range [c_lo, c_hi) of clouds of rank `rank` for warm chains
+    (chain c = layers [chain_off[c], chain_off[c+1])): cloud c goes to the rank whose
+    layer block (shard_range over all layers) holds the cloud's first layer, so ranks get
+    whole clouds and about the same number of layers."""
+    off = np.asarray(chain_off, dtype=np.int64)
+    n = int(off[-1])
+    lo, hi = shard_range(n, world, rank)
+    starts = off[:-1]
+    c_lo = int(np.searchsorted(starts, lo, side="left"))
+    c_hi = int(np.searchsorted(starts, hi, side="left")) if rank < world - 1 else len(starts)
+    return c_lo, c_hi
+
+
+def solve_chains_sharded(layers, chain_off, solve_fn: Callable, n_lev: int, device=None):
+    """Warm chains over ranks: this rank solves its clouds (chain_shard) with
+    `solve_fn(layers_subset, local_chain_off) -> (pops, status)`; returns
+    (pops, status, (first layer, last layer + 1), totals) for the local block."""
+    import torch.distributed as td
+    world = td.get_world_size() if td.is_initialized() else 1
+    rank = td.get_rank() if td.is_initialized() else 0
+    off = np.asarray(chain_off, dtype=np.int64)
+    c_lo, c_hi = chain_shard(off, world, rank)
+    l_lo, l_hi = int(off[c_lo]), int(off[c_hi])
+    if l_hi > l_lo:
+        pops, status = solve_fn(layers.subset(np.arange(l_lo, l_hi)), (off[c_lo:c_hi + 1] - l_lo).astype(np.int32))
+    else:
+        pops, status = np.zeros((0, n_lev)), np.zeros(0, dtype=abi.STATUS_DTYPE)
+    return pops, status, (l_lo, l_hi), reduce_status(status, device)
 
 
 def _default_device(device):

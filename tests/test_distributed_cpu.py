@@ -66,3 +66,42 @@ def test_gloo_world2_matches_single_process(tmp_path, name, nl):
     assert got["totals"][1] == (st["converged"] == 0).sum()
     assert got["relmax"][0] == st["rel_error"].max()
     assert np.array_equal(got["dev_tot"], [st["iterations"].sum(), (st["converged"] == 0).sum(), st["rel_error"].max()])
+
+
+def test_chain_shard_whole_clouds_balanced():
+    off = np.array([0, 5, 5, 9, 30, 31, 40, 64])
+    for w in (1, 2, 3, 4, 8):
+        spans = [dist.chain_shard(off, w, r) for r in range(w)]
+        assert spans[0][0] == 0 and spans[-1][1] == len(off) - 1
+        assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+
+
+def _chain_worker(rank, world, port, out):
+    import torch.distributed as td
+    from oracle import oracle
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    td.init_process_group("gloo", rank=rank, world_size=world)
+    P, L, o = synth.make_problem("ph2o45_1024", nb_lay=20)
+    opts = abi.default_opts(init=abi.LVG_INIT_WARM_CHAIN, **o)
+    off = [0, 3, 9, 9, 14, 20]
+    pops, st, (lo, hi), totals = dist.solve_chains_sharded(
+        L, off, lambda sub, loff: oracle.solve_chains(P, sub, loff, opts, nthreads=1), P.mol.nb_lev)
+    np.savez(out + f".{rank}.npz", pops=pops, iters=st["iterations"], lo=lo, hi=hi, tot=np.array(totals[:2]))
+    td.barrier()
+    td.destroy_process_group()
+
+
+def test_gloo_world2_warm_chains_match_single_process(tmp_path):
+    """Whole clouds per rank reproduce the single-process chains bit for bit."""
+    from oracle import oracle
+    out = str(tmp_path / "c")
+    mp.spawn(_chain_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    P, L, o = synth.make_problem("ph2o45_1024", nb_lay=20)
+    opts = abi.default_opts(init=abi.LVG_INIT_WARM_CHAIN, **o)
+    ref, st = oracle.solve_chains(P, L, [0, 3, 9, 9, 14, 20], opts)
+    r = [np.load(out + f".{k}.npz") for k in range(2)]
+    assert r[0]["lo"] == 0 and r[0]["hi"] == r[1]["lo"] and r[1]["hi"] == 20
+    assert np.array_equal(np.concatenate([r[0]["pops"], r[1]["pops"]]), ref)
+    assert np.array_equal(np.concatenate([r[0]["iters"], r[1]["iters"]]), st["iterations"])
+    assert r[0]["tot"][0] == st["iterations"].sum()
