@@ -756,10 +756,12 @@ int launch_solve(lvg_handle *h, int nb_lay, const double *d_soa, double *d_pops,
     settle(h, s);
     const int nq = chain_off ? nb_chain : nb_lay;   // queue items
     int per_cu = h->blocks_per_cu;
-    // at most two queue items per CU (e.g. 4096 layers strong-scaled over 8 GPUs): one
-    // workgroup per CU with the CU to itself finishes the longest layers sooner (512
-    // CH3OH-A layers: 9.2 vs 9.8 ms; at 1024 layers two per CU win, 12.2 vs 13.4 ms)
-    if (nq <= 2 * h->cus) per_cu = 1;
+    // at most two independent layers per CU (e.g. 4096 layers strong-scaled over 8 GPUs):
+    // one workgroup per CU with the CU to itself finishes the longest layers sooner (512
+    // CH3OH-A layers: 9.2 vs 9.8 ms; at 1024 layers two per CU win, 12.2 vs 13.4 ms). Not
+    // for warm chains, whose items are long and even: 512 chains of 8 layers take 57.7 ms
+    // at one workgroup per CU against 39.8 ms at two.
+    if (!chain_off && nq <= 2 * h->cus) per_cu = 1;
     if (const char *e = std::getenv("LVG_BLOCKS_PER_CU")) {   // tuning/diagnostics only
         const int v = std::atoi(e);
         if (v >= 1 && v <= h->blocks_per_cu) per_cu = v;
