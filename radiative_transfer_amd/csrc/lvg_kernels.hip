@@ -151,7 +151,7 @@ struct Smem {
     double red[NW];
     int    ired[2 * NW];
     unsigned long long pkey[2 * NW];   // panel: per-wave pivot keys (|v| bits, active flag), double buffered
-    double cand[2][NW][NB + 1]; // panel: each wave's pivot candidate row and its b, double buffered
+    alignas(16) double cand[2][NW][NB + 2]; // panel: each wave's pivot candidate row and its b, double buffered
     int    candp[2][NW];        // its physical row
     double L11[NB][NB + 1];
     alignas(16) double Ub[2][NB][WB + 2];   // U rows of one chunk across the block column (by chunk parity)
@@ -778,7 +778,8 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
             }
             if (act && lp == wmin) {               // this wave's candidate publishes its row
 #pragma unroll
-                for (int j = 0; j < NB; j++) if (j >= c) sm.cand[buf][w][j] = rw[j];
+                for (int j = 0; j < NB; j += 2)         // 16-byte stores from column c & ~1
+                    if (j + 1 >= c) *reinterpret_cast<double2 *>(&sm.cand[buf][w][j]) = make_double2(rw[j], rw[j + 1]);
                 sm.cand[buf][w][NB] = rb;
             }
             __syncthreads();                       // one barrier per column
@@ -799,9 +800,17 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
                 ww = better ? i : ww;
             }
             const bool owner = act && lp == lmin;
-            const double *prow = sm.cand[buf][ww];
+            const double *prow0 = sm.cand[buf][ww];
+            double prow[NB];
+#pragma unroll
+            for (int j = 0; j < NB; j += 2)             // 16-byte reads from column c & ~1
+                if (j + 1 >= c) {
+                    const double2 v = *reinterpret_cast<const double2 *>(prow0 + j);
+                    prow[j] = v.x;
+                    prow[j + 1] = v.y;
+                }
             const double piv = prow[c];
-            const double bc = prow[NB];
+            const double bc = prow0[NB];
             if (owner) { act = false; lp = c; }
             else if (lp == c) lp = lmin;
             if (act) {
