@@ -443,6 +443,9 @@ __device__ __forceinline__ void load_rule_table(const LvgDevProblem &P, Smem &sm
 #ifndef LVG_CLS_LDS
 #define LVG_CLS_LDS 1                 // pair classes staged in LDS for the collision build
 #endif
+#ifndef LVG_COLL_DEFER
+#define LVG_COLL_DEFER 1              // collision build: a batch's stores issued behind the next batch's loads
+#endif
 #ifndef LVG_COLL_PU
 #define LVG_COLL_PU 4                 // 16x16 pair tiles per batch of the collision build
 #endif
@@ -470,6 +473,26 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
     // the arithmetic and the stores (loads never wait behind stores that might alias)
     constexpr int PU = LVG_COLL_PU, TG = BT / 256;    // TG groups of 256 threads, PU tiles each
     const int tg = t >> 8;
+    // the K/B stores of a batch are issued behind the next batch's loads: vmcnt counts
+    // loads and stores in order, so a load issued after a store waits for it
+    double wk0[PU], wk1[PU], wb0[PU], wb1[PU];
+    int wf[PU], ws[PU];
+#pragma unroll
+    for (int u = 0; u < PU; u++) wf[u] = -1;
+    auto flush = [&]() {
+#pragma unroll
+        for (int u = 0; u < PU; u++) {
+            if (wf[u] >= 0) {
+                const int f = wf[u], s2 = ws[u];
+                K[s2 * N + f] = wk0[u];
+                K[f * N + s2] = wk1[u];
+                if (B) {
+                    B[s2 * N + f] = wb0[u];
+                    B[f * N + s2] = wb1[u];
+                }
+            }
+        }
+    };
     for (int q0 = 0; q0 < ntiles; q0 += PU * TG) {
         int pc[PU], fc[PU], sc[PU], cls[PU];
 #pragma unroll
@@ -511,8 +534,10 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
                 }
             }
         }
+        if (LVG_COLL_DEFER) flush();            // the previous batch's stores, behind this batch's loads
 #pragma unroll
         for (int u = 0; u < PU; u++) {
+            wf[u] = -1;
             if (pc[u] < 0) continue;
             const int cl = cls[u], f = fc[u], s = sc[u];
             const int grp = sm.tgrp[cl];
@@ -538,14 +563,16 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
                 if (dE > MIN_COLLISION_RATE) uE = dE * lvg_exp(de * CM_INVERSE_TO_KELVINS / Te) * gf[u] / gs[u];
                 else dE = 0.;
             }
-            K[s * N + f] = dn + dE;
-            K[f * N + s] = un + uE;
-            if (B) {
-                B[s * N + f] = 0.5 * af[u] + dn;
-                B[f * N + s] = un;
-            }
+            wk0[u] = dn + dE;
+            wk1[u] = un + uE;
+            wb0[u] = 0.5 * af[u] + dn;
+            wb1[u] = un;
+            wf[u] = f;
+            ws[u] = s;
         }
+        if (!LVG_COLL_DEFER) flush();
     }
+    if (LVG_COLL_DEFER) flush();
     __syncthreads();
     TACC(PH_PAIRS, tq0);
     TSTAMP(tq1);
