@@ -443,6 +443,9 @@ __device__ __forceinline__ void load_rule_table(const LvgDevProblem &P, Smem &sm
 #ifndef LVG_CLS_LDS
 #define LVG_CLS_LDS 1                 // pair classes staged in LDS for the collision build
 #endif
+#ifndef LVG_U_DEFER
+#define LVG_U_DEFER 0                 // 1: LU U stores issued behind the next step's loads (121 VGPRs spill: slower)
+#endif
 #ifndef LVG_COLL_DEFER
 #define LVG_COLL_DEFER 1              // collision build: a batch's stores issued behind the next batch's loads
 #endif
@@ -1066,6 +1069,19 @@ __device__ __forceinline__ void back_substitute(const double *A, int N, const do
 
 __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Smem &sm, const LuSrc &src, const bool FUSED) {
     const int t = threadIdx.x;
+    // U values of the last TRSM, stored to A (for the back substitution only) behind the
+    // next step's loads: vmcnt counts loads and stores in order
+    double ux[TC / 2];
+    int64_t uo[TC / 2];
+#pragma unroll
+    for (int q = 0; q < TC / 2; q++) uo[q] = -1;
+    auto flush_u = [&]() {
+#pragma unroll
+        for (int q = 0; q < TC / 2; q++) {
+            if (uo[q] >= 0) A[uo[q]] = ux[q];
+            uo[q] = -1;
+        }
+    };
     const int rg = t >> 3, cg = t & 7;   // tile rows TR*rg.., columns TC*cg..
     double s_acc = (t == 0) ? 1. : 0.;             // residual row t (FUSED)
     for (int i = t; i < N; i += BT) { sm.perm[i] = i; sm.pos[i] = i; }
@@ -1253,6 +1269,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
 #pragma unroll
                 for (int m = 0; m < NB; m++) lrow[m] = (la && m < nb) ? sm.pu.P[la ? trow : 0][m] : 0.;
             }
+            if (LVG_U_DEFER) flush_u();
             // ---- pivot rows of chunk kk (logical kk..kk+nb-1): their current values
             //      in this block column -> Ub (owners write from registers). For an
             //      earlier block's chunk they are tile rows kk.. (logical order as of
@@ -1314,7 +1331,11 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
 #pragma unroll
                     for (int q = 0; q < TC / 2; q++) {
                         const int c = (WB / 4) * w + (l >> 4) + 4 * q;
-                        if (c >= jlo && c < wJ) { sm.Ub[ub][r][c] = x[q]; A[prow + c] = x[q]; }
+                        if (c >= jlo && c < wJ) {
+                            sm.Ub[ub][r][c] = x[q];
+                            if (LVG_U_DEFER) { uo[q] = prow + c; ux[q] = x[q]; }
+                            else A[prow + c] = x[q];
+                        }
                     }
                 }
             }
@@ -1387,6 +1408,10 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             if (!(LVG_UB2 && kk + NB < c0)) __syncthreads();
             TACC(PH_GEMM, tp3);
         }
+    }
+    if (LVG_U_DEFER) {
+        flush_u();
+        __syncthreads();          // the back substitution reads U rows other threads stored
     }
     back_substitute(A, N, b, sm);
     double emax = 0.;
