@@ -131,7 +131,11 @@ constexpr double MIN_LINE_OPACITY      = 1.e-99;
 #define LVG_OCC 2                     // resident workgroups per CU solve_kernel is built for
 #endif
 constexpr int YCAP = (LVG_OCC >= 3 || LVG_BIG) ? 1 : 2048;   // line terms kept in LDS when 2*nb_lines <= YCAP
-constexpr int TC = 4;                 // columns per thread in the LU register tile (TR rows x TC)
+#ifndef LVG_TC
+#define LVG_TC 4
+#endif
+constexpr int TC = LVG_TC;            // columns per thread in the LU register tile (TR rows x TC); 4 or 2
+static_assert(TC == 4 || TC == 2, "register tile width");
 constexpr int TR = NMAX * 8 / BT;     // tile rows per thread: the BT/8 row groups cover NMAX
 static_assert(TR * (BT / 8) >= NMAX && TR % 2 == 0, "the register tiles cover every row");
 constexpr int WB = 8 * TC;            // LU block-column width
@@ -1114,18 +1118,24 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                 }
         } else {
             int li[TR][TC];
-            static_assert(TC == 4, "vector block load assumes 4 columns per thread");
             if ((N & 3) == 0 && TC * cg + TC <= wJ) {
-                // whole 4-column segments, 32-byte aligned: 2 x 16-byte K loads, 1 x 16-byte li load
+                // whole TC-column segments, aligned: 16-byte K loads, one li load
 #pragma unroll
                 for (int i = 0; i < TR; i++) {
                     const bool ok = TR * rg + i < N;
                     const int64_t o = (int64_t)(ok ? prow[i] : 0) * N + c0 + TC * cg;
-                    const double2 k0 = ok ? reinterpret_cast<const double2 *>(src.K + o)[0] : make_double2(0., 0.);
-                    const double2 k1 = ok ? reinterpret_cast<const double2 *>(src.K + o)[1] : make_double2(0., 0.);
-                    const int4 l4 = ok ? *reinterpret_cast<const int4 *>(src.li + o) : make_int4(-1, -1, -1, -1);
-                    acc[i][0] = k0.x; acc[i][1] = k0.y; acc[i][2] = k1.x; acc[i][3] = k1.y;
-                    li[i][0] = l4.x; li[i][1] = l4.y; li[i][2] = l4.z; li[i][3] = l4.w;
+                    if constexpr (TC == 4) {
+                        const double2 k0 = ok ? reinterpret_cast<const double2 *>(src.K + o)[0] : make_double2(0., 0.);
+                        const double2 k1 = ok ? reinterpret_cast<const double2 *>(src.K + o)[1] : make_double2(0., 0.);
+                        const int4 l4 = ok ? *reinterpret_cast<const int4 *>(src.li + o) : make_int4(-1, -1, -1, -1);
+                        acc[i][0] = k0.x; acc[i][1] = k0.y; acc[i][2] = k1.x; acc[i][3] = k1.y;
+                        li[i][0] = l4.x; li[i][1] = l4.y; li[i][2] = l4.z; li[i][3] = l4.w;
+                    } else {
+                        const double2 k0 = ok ? reinterpret_cast<const double2 *>(src.K + o)[0] : make_double2(0., 0.);
+                        const int2 l2 = ok ? *reinterpret_cast<const int2 *>(src.li + o) : make_int2(-1, -1);
+                        acc[i][0] = k0.x; acc[i][1] = k0.y;
+                        li[i][0] = l2.x; li[i][1] = l2.y;
+                    }
                 }
             } else {
 #pragma unroll
