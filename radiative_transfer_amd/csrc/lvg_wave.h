@@ -19,6 +19,12 @@
 // order; results are bit-identical, which tests/test_gpu_parity.py checks.
 #pragma once
 
+#ifndef LVG_WAVE_CLAMP
+#define LVG_WAVE_CLAMP 1              // assembly operands read unconditionally (clamped indices)
+#endif
+#ifndef LVG_WAVE_ACCEL_BATCH
+#define LVG_WAVE_ACCEL_BATCH 1        // Ng sums: ring reads of 8 levels per round trip
+#endif
 constexpr int WYCAP = 512;        // line terms y per wave kept in LDS (host checks 2*nb_lines <= WYCAP)
 constexpr int WGRID_CAP = 1024;   // escape + overlap grid doubles copied to LDS (host checks)
 constexpr int WNMAX = 64;
@@ -461,11 +467,33 @@ __device__ __forceinline__ void wave_accel_step(Ctl &C, Slot &S, int N, WaveLaye
         const double *ri = ring(S.res, C.hr, i + 1, N);
         const double *rj = (j >= 0) ? ring(S.res, C.hr, j + 1, N) : nullptr;
         double a = 0.;
+#if LVG_WAVE_ACCEL_BATCH
+        // the ring reads of 8 levels issued together (one round trip per block), the sum
+        // still taken for k ascending
+        const double *rjj = (j >= 0) ? rj : ri;
+        for (int k0 = 0; k0 < N; k0 += 8) {
+            double pv[8], r0v[8], riv[8], rjv[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int k = (k0 + u < N) ? k0 + u : k0;
+                pv[u] = p0[k]; r0v[u] = r0[k]; riv[u] = ri[k]; rjv[u] = rjj[k];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                if (k0 + u < N) {
+                    double w = pv[u] + 1.e-99;
+                    double num = (j >= 0) ? (r0v[u] - riv[u]) * (r0v[u] - rjv[u]) : (r0v[u] - riv[u]) * r0v[u];
+                    a = a + num / (w * w);
+                }
+            }
+        }
+#else
         for (int k = 0; k < N; k++) {
             double w = p0[k] + 1.e-99;
             double num = (j >= 0) ? (r0[k] - ri[k]) * (r0[k] - rj[k]) : (r0[k] - ri[k]) * r0[k];
             a = a + num / (w * w);
         }
+#endif
         sm.hist_acc[t] = a;
     }
     wave_sync();
@@ -504,7 +532,16 @@ __device__ __forceinline__ void wave_accel_step(Ctl &C, Slot &S, int N, WaveLaye
     const double sum = sm.hist_acc[31];
     for (int k = t; k < N; k += 64) {
         double a = (1. - sum) * p0[k];
+#if LVG_WAVE_ACCEL_BATCH
+        double pv[4];                   // np <= 4 (accel_nb <= 5, checked by the host)
+#pragma unroll
+        for (int i = 0; i < 4; i++) pv[i] = (i < np) ? ring(S.prev, C.hp, i + 1, N)[k] : 0.;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            if (i < np) a = a + sm.hist_acc[16 + i] * pv[i];
+#else
         for (int i = 0; i < np; i++) a = a + sm.hist_acc[16 + i] * ring(S.prev, C.hp, i + 1, N)[k];
+#endif
         sm.pold[k] = a;
     }
     wave_sync();
@@ -632,8 +669,15 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
 #pragma unroll
                     for (int u = 0; u < 8; u++) {
                         const int r = r0 + u;
-                        kc[u] = (r < N) ? K[r * ldk + d] : 0.;
-                        lc[u] = (il && r < N) ? li[r * ldk + d] : -1;
+                        if (LVG_WAVE_CLAMP) {   // unconditional LDS reads (row 0 stands in past N)
+                            const int rr = (r < N) ? r : 0;
+                            kc[u] = K[rr * ldk + d];
+                            const int lv = li[rr * ldk + d];
+                            lc[u] = (il && r < N) ? lv : -1;
+                        } else {
+                            kc[u] = (r < N) ? K[r * ldk + d] : 0.;
+                            lc[u] = (il && r < N) ? li[r * ldk + d] : -1;
+                        }
                     }
 #pragma unroll
                     for (int u = 0; u < 8; u++) yc[u] = sm.y[lc[u] >= 0 ? lc[u] : 0];
@@ -659,9 +703,17 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
                     const int j = j0 + u;
-                    kc[u] = (j < N) ? K[row * ldk + j] : 0.;
-                    lc[u] = (j < N) ? li[row * ldk + j] : -1;
-                    pc[u] = (j < N) ? sm.pold[j] : 0.;
+                    if (LVG_WAVE_CLAMP) {
+                        const int jj = (j < N) ? j : 0;
+                        kc[u] = K[row * ldk + jj];
+                        const int lv = li[row * ldk + jj];
+                        lc[u] = (j < N) ? lv : -1;
+                        pc[u] = sm.pold[j];        // j < NM <= WNMAX
+                    } else {
+                        kc[u] = (j < N) ? K[row * ldk + j] : 0.;
+                        lc[u] = (j < N) ? li[row * ldk + j] : -1;
+                        pc[u] = (j < N) ? sm.pold[j] : 0.;
+                    }
                 }
 #pragma unroll
                 for (int u = 0; u < 8; u++) yc[u] = sm.y[lc[u] >= 0 ? lc[u] : 0];

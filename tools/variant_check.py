@@ -1,11 +1,14 @@
-"""Exactness probe for a library variant (LVG_LIB_PATH): 128 CH3OH-A layers against the oracle."""
+"""Exactness probe for a library variant (LVG_LIB_PATH): a layer subset of a workload
+(default 128 CH3OH-A layers; argv: workload, layers) against the oracle."""
 import sys
 import numpy as np
 sys.path.insert(0, "/root/repo")
 from radiative_transfer_amd import synth, abi, native
 from oracle import oracle
 
-P, L, o = synth.make_problem("ch3oha256_4096", nb_lay=128)
+name = sys.argv[1] if len(sys.argv) > 1 else "ch3oha256_4096"
+nl = int(sys.argv[2]) if len(sys.argv) > 2 else 128
+P, L, o = synth.make_problem(name, nb_lay=nl)
 opts = abi.default_opts(**o)
 s = native.LvgSolver(P)
 pg, sg = s.solve_layers(L, opts)
