@@ -22,6 +22,9 @@
 #ifndef LVG_WAVE_CLAMP
 #define LVG_WAVE_CLAMP 1              // assembly operands read unconditionally (clamped indices)
 #endif
+#ifndef LVG_WAVE_OPAQUE_N
+#define LVG_WAVE_OPAQUE_N 1
+#endif
 #ifndef LVG_WAVE_ACCEL_BATCH
 #define LVG_WAVE_ACCEL_BATCH 1        // Ng sums: ring reads of 8 levels per round trip
 #endif
@@ -640,6 +643,11 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
     for (;;) {
         double a[NM];
         double eq = 0.;
+        // N through an opaque SGPR copy each pass: otherwise the compiler hoists every
+        // N-derived lane mask and K address of the unrolled loops out of the layer loop and
+        // spills them (v_writelane / v_readlane + s_nop on every use)
+        int N = P.N;
+        if (LVG_WAVE_OPAQUE_N && NM <= 32) asm volatile("" : "+s"(N));   // measured: helps NM=24, hurts NM=48
         if (boundary) {
             TSTAMP(tbd);
             wave_boundary_rows<NM>(S.A, N, a);
