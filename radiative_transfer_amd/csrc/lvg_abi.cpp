@@ -568,6 +568,8 @@ int ensure_workspace(lvg_handle *h, int slots) {
     const int N = h->N;
     const int lines = std::max(h->P.plain.nb_lines, h->P.overlap.nb_lines);
     int64_t stride = 2LL * N * N + 2LL * LVG_HIST_SLOTS * N + 3LL * N + 2LL * lines + 64;
+    // wave kernel: per-layer line invariants after the y region (wave_line_invariants)
+    if (N <= LVG_WAVE_NMAX) stride += (int64_t)LVG_WAVE_INV_FIELDS * lines;
     stride = (stride + 31) & ~31LL;
     size_t bytes = (size_t)stride * slots * sizeof(double);
     if (bytes > h->ws_bytes) {

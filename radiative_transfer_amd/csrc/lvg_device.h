@@ -21,6 +21,8 @@
 #define LVG_MAX_COMBOS   16
 #define LVG_MAX_DUST     4
 #define LVG_HIST_SLOTS   8      // ring slots for prev_level_pop / residual_list
+#define LVG_WAVE_INV_FIELDS 20  // wave kernel: per-layer line-invariant doubles per unit (slot tail)
+#define LVG_WAVE_NMAX    64     // wave kernel level cap (slots carry the invariant records up to here)
 
 struct LvgTermTable {
     int8_t table[LVG_MAX_CLASSES][LVG_MAX_TERMS];  // neutral terms, -1 = none

@@ -25,6 +25,9 @@
 #ifndef LVG_WAVE_OPAQUE_N
 #define LVG_WAVE_OPAQUE_N 1
 #endif
+#ifndef LVG_WAVE_LINE_INV
+#define LVG_WAVE_LINE_INV 1           // line terms from per-layer invariant records (wave_line_invariants)
+#endif
 #ifndef LVG_WAVE_ACCEL_BATCH
 #define LVG_WAVE_ACCEL_BATCH 1        // Ng sums: ring reads of 8 levels per round trip
 #endif
@@ -219,6 +222,211 @@ __device__ __forceinline__ double esc_sum(const EscIdx &o, const double (&v)[4])
     const double t = o.t, u = o.u;
     double e = v[0] * (1. - t) * (1. - u) + v[1] * t * (1. - u) + v[2] * (1. - t) * u + v[3] * u * t;
     return e > 1. ? 1. : (e < 0. ? 0. : e);
+}
+
+// ---- per-layer line invariants -----------------------------------------------------
+// Everything in intensity_single / intensity_pair that does not depend on the
+// populations is fixed for the whole layer: the unit's line indices and Einstein
+// coefficients, c = n_mol / (8 pi v_w E^3), the dust opacity and from it delta, its
+// escape-grid interval (k, t) and log10(delta)'s overlap-grid interval (m, y), and for a
+// pair the frequency offset dx with its overlap-grid intervals for +dx and -dx. They are
+// computed once per layer (same expressions, same results) into the wave's slot as
+// structure-of-arrays records (field f of unit q at inv[f * cap + q]), so an iteration
+// reads one coalesced record per unit: one global round trip instead of the dependent
+// unit -> line data -> level energies chain, and no dust sum, log10 or delta / dx
+// bisection per iteration.
+enum { WI_N1, WI_U1, WI_L1, WI_A1, WI_B1, WI_C, WI_EK, WI_ET, WI_PLAIN,
+       WI_N2 = WI_PLAIN, WI_U2, WI_L2, WI_A2, WI_B2, WI_DX, WI_OM, WI_OY, WI_AN, WI_AP, WI_BN, WI_BP, WI_ALL };
+static_assert(WI_ALL == LVG_WAVE_INV_FIELDS, "host reserves LVG_WAVE_INV_FIELDS doubles per line");
+
+__device__ __forceinline__ void ov_interval(const double *g, int n, double x, int &j, double &w) {
+    j = locate_index(g, n, x);
+    if (j < 0) { j = 0; w = 0.; }
+    else if (j > n - 2) { j = n - 2; w = 1.; }
+    else w = (x - g[j]) / (g[j + 1] - g[j]);
+}
+
+__device__ __forceinline__ void wave_line_invariants(const LvgDevProblem &P, const EscGrids &G, const LvgModeLines &M,
+                                                     const WaveLayer &sm, bool ov, double *inv, int cap) {
+    for (int q = lane_id(); q < M.nb_units; q += 64) {
+        const int n1 = M.unit_l0[q];
+        const double energy = M.line_e[n1];
+        const double c = sm.nmol / (EIGHT_PI * sm.vw * energy * energy * energy);
+        const double delta = fabs(sm.vgrad) / (sm.vw * dust_opacity(P, M, sm, n1));
+        const int u1 = M.line_u[n1], l1 = M.line_l[n1];
+        int k;
+        double t;
+        ov_interval(G.ed, P.esc_nd, delta, k, t);   // esc_index's delta part
+        inv[WI_N1 * cap + q] = n1;
+        inv[WI_U1 * cap + q] = u1;
+        inv[WI_L1 * cap + q] = l1;
+        inv[WI_A1 * cap + q] = M.line_aul[n1];
+        inv[WI_B1 * cap + q] = M.line_alu[n1];
+        inv[WI_C * cap + q] = c;
+        inv[WI_EK * cap + q] = k;
+        inv[WI_ET * cap + q] = t;
+        if (!ov) continue;
+        const int n2 = M.unit_l1[q];
+        inv[WI_N2 * cap + q] = n2;
+        if (n2 < 0) continue;
+        const int u2 = M.line_u[n2], l2 = M.line_l[n2];
+        double dx = (P.energy[u1] - P.energy[l1] - P.energy[u2] + P.energy[l2]) * SPEED_OF_LIGHT / (energy * sm.vw);
+        if (sm.vgrad < 0.) dx *= -1.;
+        int m, an, bn;
+        double y, ap, bp;
+        ov_interval(G.old, P.ov_nd, lvg_log10(delta), m, y);
+        ov_interval(G.odx, P.ov_ndx, dx, an, ap);
+        ov_interval(G.odx, P.ov_ndx, -dx, bn, bp);
+        inv[WI_U2 * cap + q] = u2;
+        inv[WI_L2 * cap + q] = l2;
+        inv[WI_A2 * cap + q] = M.line_aul[n2];
+        inv[WI_B2 * cap + q] = M.line_alu[n2];
+        inv[WI_DX * cap + q] = dx;
+        inv[WI_OM * cap + q] = m;
+        inv[WI_OY * cap + q] = y;
+        inv[WI_AN * cap + q] = an;
+        inv[WI_AP * cap + q] = ap;
+        inv[WI_BN * cap + q] = bn;
+        inv[WI_BP * cap + q] = bp;
+    }
+}
+
+// plain scheme from the invariants: WUB units per lane per pass, stores last
+__device__ __forceinline__ void wave_line_terms_plain_inv(const LvgDevProblem &P, const EscGrids &G,
+                                                          const LvgModeLines &M, WaveLayer &sm, const double *inv,
+                                                          int cap) {
+    const int t = lane_id(), U = M.nb_units;
+    constexpr int B = 4;
+    for (int q0 = t; q0 < U; q0 += 64 * B) {
+        double f[B][WI_PLAIN];
+#pragma unroll
+        for (int b = 0; b < B; b++) {
+            const int q = (q0 + 64 * b < U) ? q0 + 64 * b : q0;
+#pragma unroll
+            for (int i = 0; i < WI_PLAIN; i++) f[b][i] = inv[i * cap + q];
+        }
+        EscIdx ix[B];
+        double em[B], op[B], tv[B][4];
+#pragma unroll
+        for (int b = 0; b < B; b++) {
+            const double c = f[b][WI_C];
+            em[b] = c * f[b][WI_A1] * sm.pold[(int)f[b][WI_U1]];
+            op[b] = c * f[b][WI_B1] * sm.pold[(int)f[b][WI_L1]] - em[b] + MIN_LINE_OPACITY;
+            if (op[b] < 0.) op[b] *= INV_TRANS_FACTOR;
+            const double gamma = fabs(sm.vgrad) / (sm.vw * op[b]);
+            ix[b].k = (int)f[b][WI_EK];
+            ix[b].t = f[b][WI_ET];
+            ov_interval(G.eg, P.esc_ng, gamma, ix[b].l, ix[b].u);   // esc_index's gamma part
+        }
+#pragma unroll
+        for (int b = 0; b < B; b++) esc_load(P, ix[b], tv[b]);
+#pragma unroll
+        for (int b = 0; b < B; b++) {
+            if (q0 + 64 * b < U) {
+                const double I = em[b] / op[b] * esc_sum(ix[b], tv[b]);
+                const int n = (int)f[b][WI_N1];
+                sm.y[2 * n] = f[b][WI_A1] * (1. + I);
+                sm.y[2 * n + 1] = f[b][WI_B1] * I;
+            }
+        }
+    }
+}
+
+// overlap scheme from the invariants (intensity_single / intensity_pair sequences)
+__device__ __forceinline__ void wave_line_terms_overlap_inv(const LvgDevProblem &P, const EscGrids &G,
+                                                            const LvgModeLines &M, WaveLayer &sm, const double *inv,
+                                                            int cap) {
+    const double max_dx = 4.;
+    const double *pop = sm.pold;
+    for (int q = lane_id(); q < M.nb_units; q += 64) {
+        double f[WI_ALL];
+#pragma unroll
+        for (int i = 0; i < WI_ALL; i++) f[i] = inv[i * cap + q];
+        const int n1 = (int)f[WI_N1], n2 = (int)f[WI_N2];
+        const double c0 = f[WI_C], a1 = f[WI_A1], b1 = f[WI_B1];
+        if (n2 < 0) {
+            const double emiss = c0 * a1 * pop[(int)f[WI_U1]];
+            double opac = c0 * b1 * pop[(int)f[WI_L1]] - emiss + MIN_LINE_OPACITY;
+            if (opac < 0.) opac *= INV_TRANS_FACTOR;
+            const double gamma = fabs(sm.vgrad) / (sm.vw * opac);
+            EscIdx ix;
+            ix.k = (int)f[WI_EK];
+            ix.t = f[WI_ET];
+            ov_interval(G.eg, P.esc_ng, gamma, ix.l, ix.u);
+            double tv[4];
+            esc_load(P, ix, tv);
+            const double I = emiss / opac * esc_sum(ix, tv);
+            sm.y[2 * n1] = a1 * (1. + I);
+            sm.y[2 * n1 + 1] = b1 * I;
+            continue;
+        }
+        const int u1 = (int)f[WI_U1], l1 = (int)f[WI_L1], u2 = (int)f[WI_U2], l2 = (int)f[WI_L2];
+        const double a2 = f[WI_A2], b2 = f[WI_B2], dx = f[WI_DX];
+        const double em1 = c0 * a1 * pop[u1];
+        double op1 = c0 * (b1 * pop[l1] - a1 * pop[u1]) + MIN_LINE_OPACITY;
+        const double em2 = c0 * a2 * pop[u2];
+        double op2 = c0 * (b2 * pop[l2] - a2 * pop[u2]) + MIN_LINE_OPACITY;
+        if (op1 < 0.) op1 *= INV_TRANS_FACTOR;
+        if (op2 < 0.) op2 *= INV_TRANS_FACTOR;
+        const double g1 = fabs(sm.vgrad) / (sm.vw * op1), g2 = fabs(sm.vgrad) / (sm.vw * op2);
+        const bool near = fabs(dx) < max_dx, far = fabs(dx) > max_dx - 0.5;
+        double ep1 = 0., ep2 = 0., ep01 = 0., ep02 = 0., q1 = 0., q2 = 0.;
+        if (near) {
+            OvIdx A, B;
+            A.m = B.m = (int)f[WI_OM];
+            A.y = B.y = f[WI_OY];
+            A.n = (int)f[WI_AN]; A.p = f[WI_AP];
+            B.n = (int)f[WI_BN]; B.p = f[WI_BP];
+            ov_interval(G.og, P.ov_ng, g1, A.l, A.u);
+            ov_interval(G.ogr, P.ov_ngr, g2 / g1, A.k, A.t);
+            ov_interval(G.og, P.ov_ng, g2, B.l, B.u);
+            ov_interval(G.ogr, P.ov_ngr, g1 / g2, B.k, B.t);
+            double v1[16], v2[16], w1[16], w2[16];
+            ov_load(P, P.ov_p1, A, v1);
+            ov_load(P, P.ov_p1, B, v2);
+            ov_load(P, P.ov_p2, A, w1);
+            ov_load(P, P.ov_p2, B, w2);
+            ep1 = ov_sum(A, v1);
+            ep2 = ov_sum(B, v2);
+            q1 = ov_sum(A, w1);
+            q2 = ov_sum(B, w2);
+        }
+        if (far) {
+            EscIdx A, B;
+            A.k = B.k = (int)f[WI_EK];
+            A.t = B.t = f[WI_ET];
+            ov_interval(G.eg, P.esc_ng, g1, A.l, A.u);
+            ov_interval(G.eg, P.esc_ng, g2, B.l, B.u);
+            double v1[4], v2[4];
+            esc_load(P, A, v1);
+            esc_load(P, B, v2);
+            ep01 = esc_sum(A, v1);
+            ep02 = esc_sum(B, v2);
+        }
+        double c = c0;
+        if (fabs(dx) > max_dx) { ep1 = ep01; ep2 = ep02; }
+        else if (far) {
+            c = 2. * (max_dx - fabs(dx));
+            ep1 = ep01 * (1. - c) + ep1 * c;
+            ep2 = ep02 * (1. - c) + ep2 * c;
+        }
+        double i1 = em1 / op1 * ep1;
+        double i2 = em2 / op2 * ep2;
+        if (near) {
+            ep1 = q1;
+            ep2 = q2;
+            if (far) {
+                c = 2. * (max_dx - fabs(dx));
+                ep1 *= c; ep2 *= c;
+            }
+            i1 += em2 / op2 * ep1;
+            i2 += em1 / op1 * ep2;
+        }
+        sm.y[2 * n1] = a1 * (1. + i1);
+        sm.y[2 * n1 + 1] = b1 * i1;
+        sm.y[2 * n2] = a2 * (1. + i2);
+        sm.y[2 * n2 + 1] = b2 * i2;
+    }
 }
 
 // plain scheme: WUB single-line units per lane per pass (intensity_single), stores last
@@ -623,7 +831,11 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
     lvg_layer_status *st = reinterpret_cast<lvg_layer_status *>(Lc.status) + l;
     const bool need_boundary = (Lc.init != LVG_INIT_GIVEN);
     wave_collisions(P, sh, sm, K, ldk, (need_boundary && !from_prev) ? S.A : nullptr);
-    if (need_boundary && !from_prev) wave_sync_global();   // B is read across lanes
+    // line invariants after the y region of the slot (host: ensure_workspace)
+    const int inv_cap = P.plain.nb_lines > P.overlap.nb_lines ? P.plain.nb_lines : P.overlap.nb_lines;
+    double *inv = S.y + 2 * inv_cap + 64;
+    if (LVG_WAVE_LINE_INV) wave_line_invariants(P, G, M, sm, Lc.line_overlap != 0, inv, inv_cap);
+    if (LVG_WAVE_LINE_INV || (need_boundary && !from_prev)) wave_sync_global();   // B is read across lanes
     else wave_sync();
     TACC(PH_SETUP, ts0);
     if (!need_boundary) {
@@ -658,7 +870,10 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
             TACC(PH_CTL, tc0);
             TSTAMP(tl0);
             // line terms y (compute_line_terms)
-            if (Lc.line_overlap) wave_line_terms_overlap(P, G, M, sm);
+            if (LVG_WAVE_LINE_INV) {
+                if (Lc.line_overlap) wave_line_terms_overlap_inv(P, G, M, sm, inv, inv_cap);
+                else wave_line_terms_plain_inv(P, G, M, sm, inv, inv_cap);
+            } else if (Lc.line_overlap) wave_line_terms_overlap(P, G, M, sm);
             else wave_line_terms_plain(P, G, M, sm);
             wave_sync();
             TACC(PH_LINES, tl0);
