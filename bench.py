@@ -212,12 +212,13 @@ def main():
     if multi:
         td.barrier()
     torch.cuda.synchronize()
-    kern_ms = []
+    kern_ms, coll_ms = [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         glob = step()
         ms, _ = solver.last_kernel_time()
         kern_ms.append(ms)
+        coll_ms.append(solver.last_coll_time())
     torch.cuda.synchronize()
     if multi:
         td.barrier()
@@ -259,6 +260,9 @@ def main():
                     "frac": achieved / PEAK_HBM_GBS}
         roof.update({"traffic": traffic, "traffic_source": tsrc if traffic else None,
                      "kernel": kernel, "kernel_ms": kms,
+                     # collision operators of the batch, built ahead by lvg::coll_kernel (in the
+                     # step time, not in kernel_ms; 0 when each layer builds its own in-kernel)
+                     "coll_kernel_ms": float(np.mean(coll_ms)),
                      "flops_per_unit": flops_per_layer_iteration(N),
                      "hbm_model_bytes_per_unit": bytes_per_layer_iteration(N), "units_per_launch": per_launch,
                      "fp64_frac": flops_per_layer_iteration(N) * per_launch / (kms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS,

@@ -330,6 +330,13 @@ int         lvg_lim_luminosity(lvg_handle *h, const lvg_layers *layers, const lv
  * solve kernel(s) and their count. */
 int         lvg_last_kernel_time(const lvg_handle *h, double *ms, int *nb_launches);
 
+/* Milliseconds of the collision-operator kernel (coll_kernel) that ran ahead of
+ * the solve kernel in the last lvg_solve_layers* call, 0 if it did not run
+ * (wave kernel, warm chains, LVG_COLL_AHEAD=0 or over the memory budget). The
+ * reference builds these operators inside set_gas_param per layer
+ * (coll_rates.cpp:152-174, iteration_lvg.cpp:121-131); no reference counterpart. */
+int         lvg_last_coll_time(const lvg_handle *h, double *ms);
+
 #ifdef __cplusplus
 }
 #endif

@@ -25,6 +25,7 @@
 #include "lvg_device.h"
 
 extern "C" hipError_t lvg_launch_solve(const LvgDevProblem *P, const LvgLaunch *L, int grid, hipStream_t s);
+extern "C" hipError_t lvg_launch_coll(const LvgDevProblem *P, const LvgLaunch *L, int grid, hipStream_t s);
 extern "C" int lvg_wave_plan(int N, int nb_y, int grid_doubles, size_t lds_cap, int *wpb, size_t *dyn);
 extern "C" hipError_t lvg_wave_occupancy(int N, int wpb, size_t dyn, int *blocks_per_cu);
 extern "C" hipError_t lvg_launch_solve_wave(const LvgDevProblem *P, const LvgLaunch *L, int N, int grid, int wpb,
@@ -70,7 +71,7 @@ struct lvg_handle {
     int cus = 0, blocks_per_cu = 1;
     int big = 0;                   // N > 256: the 768-thread block kernel (lvg_kernels_big.hip)
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, evc = nullptr;   // evc: end of coll_kernel
     LvgDevProblem P{};
     std::vector<DevBuf> bufs;
     // workspace
@@ -87,11 +88,14 @@ struct lvg_handle {
     // layer scheduling order (lvg_sched.hip)
     void *d_sched = nullptr, *d_sched_tmp = nullptr;
     size_t sched_cap = 0, sched_tmp_cap = 0;
+    void *d_coll = nullptr;            // K_all, B_all of the last coll_kernel batch
+    size_t coll_cap = 0;
     // warm chains: offsets [nb_chain + 1] then queue order [nb_chain] (device + host staging)
     int *d_chain = nullptr;
     size_t chain_cap = 0;
     std::vector<int> chain_host;
-    double last_ms = 0.;
+    double last_ms = 0., last_coll_ms = 0.;
+    int last_coll = 0;
     int last_launches = 0;
     // an asynchronous lvg_solve_layers_device (caller's stream) may still be running:
     // its kernel reads the launch block, the queue counter and the workspace slots, so
@@ -680,9 +684,11 @@ void lvg_destroy(lvg_handle *h) {
     if (h->d_launch) (void)hipFree(h->d_launch);
     if (h->d_sched) (void)hipFree(h->d_sched);
     if (h->d_sched_tmp) (void)hipFree(h->d_sched_tmp);
+    if (h->d_coll) (void)hipFree(h->d_coll);
     if (h->d_chain) (void)hipFree(h->d_chain);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->evc) (void)hipEventDestroy(h->evc);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -709,6 +715,7 @@ int lvg_create(const lvg_problem *prob, int device, lvg_handle **out) {
         if (hipGetDeviceProperties(&prop, device) != hipSuccess ||
             hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
+            hipEventCreate(&h->evc) != hipSuccess ||
             hipMalloc(&h->counter, sizeof(int)) != hipSuccess)
             rc = fail(h, LVG_E_DEVICE, "device setup failed");
         else {
@@ -826,10 +833,38 @@ int launch_solve(lvg_handle *h, int nb_lay, const double *d_soa, double *d_pops,
         HIPCHECK(h, lvg_sched_order(d_soa, nb_lay, nb_lay, keys, keys2, idx, order, h->d_sched_tmp, &tmp, s));
         L.order = order;
     }
+    // independent layers on the block kernels: collision operators of the whole batch
+    // built ahead by coll_kernel into HBM (K, and B for the boundary-layer start) when
+    // they fit the budget (LVG_COLL_AHEAD=0 disables; LVG_COLL_AHEAD_GB, default 64)
+    bool coll_ahead = false;
+    if (!wave && !chain_off) {
+        const char *e = std::getenv("LVG_COLL_AHEAD");
+        const char *g = std::getenv("LVG_COLL_AHEAD_GB");
+        const double cap_gb = g ? std::atof(g) : 64.;
+        const bool need_b = o->init != LVG_INIT_GIVEN;
+        const bool b_from_k = h->P.nb_tables == h->P.nb_neutral;   // no electron tables: B = f(K)
+        const size_t nn = (size_t)nb_lay * h->N * h->N * sizeof(double);
+        const size_t nd = (size_t)nb_lay * h->N * sizeof(double);
+        const size_t bytes = nn + (need_b ? (b_from_k ? nd : nn) : 0);
+        if (!(e && e[0] == '0') && (double)bytes <= cap_gb * 1073741824.) {
+            if ((rc = grow(h, &h->d_coll, &h->coll_cap, bytes))) return rc;
+            L.kall = static_cast<const double *>(h->d_coll);
+            const double *tail = static_cast<const double *>(h->d_coll) + nn / sizeof(double);
+            L.ball = (need_b && !b_from_k) ? tail : nullptr;
+            L.bdiag = (need_b && b_from_k) ? tail : nullptr;
+            coll_ahead = true;
+        }
+    }
     const LvgLaunch *dL = nullptr;
     if ((rc = push_launch(h, L, 0, s, &dL))) return rc;
     HIPCHECK(h, hipMemsetAsync(h->counter, 0, sizeof(int), s));
     HIPCHECK(h, hipEventRecord(h->ev0, s));
+    h->last_coll = coll_ahead ? 1 : 0;
+    h->last_coll_ms = 0.;
+    if (coll_ahead) {
+        HIPCHECK(h, lvg_launch_coll(h->d_prob, dL, std::min(nb_lay, 8 * h->cus), s));
+        HIPCHECK(h, hipEventRecord(h->evc, s));
+    }
     if (wave) HIPCHECK(h, lvg_launch_solve_wave(h->d_prob, dL, h->N, grid, wpb, wdyn, s));
     else HIPCHECK(h, h->big ? lvg_launch_solve_big(h->d_prob, dL, grid, s) : lvg_launch_solve(h->d_prob, dL, grid, s));
     HIPCHECK(h, hipEventRecord(h->ev1, s));
@@ -837,7 +872,14 @@ int launch_solve(lvg_handle *h, int nb_lay, const double *d_soa, double *d_pops,
     if (!stream) {
         HIPCHECK(h, hipStreamSynchronize(s));
         float ms = 0.f;
-        (void)hipEventElapsedTime(&ms, h->ev0, h->ev1);
+        if (h->last_coll) {
+            float mc = 0.f;
+            (void)hipEventElapsedTime(&mc, h->ev0, h->evc);
+            (void)hipEventElapsedTime(&ms, h->evc, h->ev1);
+            h->last_coll_ms = mc;
+        } else {
+            (void)hipEventElapsedTime(&ms, h->ev0, h->ev1);
+        }
         h->last_ms = ms;
         h->pending = 0;
     } else {
@@ -880,11 +922,23 @@ int lvg_last_kernel_time(const lvg_handle *h, double *ms, int *nb) {
     lvg_handle *hh = const_cast<lvg_handle *>(h);
     if (hh->last_launches && hh->last_ms == 0.) {
         float f = 0.f;
-        if (hipEventSynchronize(hh->ev1) == hipSuccess && hipEventElapsedTime(&f, hh->ev0, hh->ev1) == hipSuccess)
+        float fc = 0.f;
+        if (hipEventSynchronize(hh->ev1) == hipSuccess &&
+            hipEventElapsedTime(&f, hh->last_coll ? hh->evc : hh->ev0, hh->ev1) == hipSuccess)
             hh->last_ms = f;
+        if (hh->last_coll && hipEventElapsedTime(&fc, hh->ev0, hh->evc) == hipSuccess) hh->last_coll_ms = fc;
     }
     if (ms) *ms = hh->last_ms;
     if (nb) *nb = hh->last_launches;
+    return LVG_OK;
+}
+
+int lvg_last_coll_time(const lvg_handle *h, double *ms) {
+    if (!h) return LVG_E_STATE;
+    double k = 0.;
+    int rc = lvg_last_kernel_time(h, &k, nullptr);   // settles both timings
+    if (rc) return rc;
+    if (ms) *ms = h->last_coll ? h->last_coll_ms : 0.;
     return LVG_OK;
 }
 

@@ -96,6 +96,12 @@ struct LvgLaunch {
     int64_t   ws_stride;
     int      *counter;                // work queue head
     const int *order;                 // queue position -> layer (NULL: index order)
+    // collision operators built ahead by coll_kernel (NULL: each layer builds its own):
+    // K [nb_lay][N][N] and the boundary matrix B [nb_lay][N][N] (B NULL when not needed)
+    const double *kall, *ball;
+    // without electron tables B is K + A/2 above the diagonal and K below it: then only
+    // its diagonal is stored, bdiag [nb_lay][N], and the boundary LU forms B from K
+    const double *bdiag;
     // debug probe outputs (lvg_debug_calc_new_pop)
     double   *dbg_matrix, *dbg_df, *dbg_pop_in;
     int       dbg_mode;               // 0 solve, 1 debug calc_new_pop, 2 boundary pops only

@@ -425,7 +425,8 @@ __device__ __forceinline__ void layer_setup(const LvgDevProblem &P, const LvgLau
 }
 
 // the compiled molecule rule, copied to LDS once per launch
-__device__ __forceinline__ void load_rule_table(const LvgDevProblem &P, Smem &sm) {
+template <class SM>
+__device__ __forceinline__ void load_rule_table(const LvgDevProblem &P, SM &sm) {
     for (int e = threadIdx.x; e < LVG_MAX_CLASSES * LVG_MAX_TERMS; e += BT) {
         (&sm.ttab[0][0])[e] = (&P.terms.table[0][0])[e];
         (&sm.tcombo[0][0])[e] = (&P.terms.combo[0][0])[e];
@@ -456,7 +457,8 @@ __device__ __forceinline__ void load_rule_table(const LvgDevProblem &P, Smem &sm
 #ifndef LVG_COLL_PU
 #define LVG_COLL_PU 4                 // 16x16 pair tiles per batch of the collision build
 #endif
-__device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P, Smem &sm, double *K, double *B,
+template <class SM, int PU = LVG_COLL_PU>
+__device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P, SM &sm, double *K, double *B,
                                                           bool electrons = true) {
     const int N = P.N, t = threadIdx.x;
     const double T = sm.T, Te = sm.Te;
@@ -478,7 +480,7 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
     }
     // batches of PU tiles: indices and classes, then every coefficient load, then
     // the arithmetic and the stores (loads never wait behind stores that might alias)
-    constexpr int PU = LVG_COLL_PU, TG = BT / 256;    // TG groups of 256 threads, PU tiles each
+    constexpr int TG = BT / 256;                     // TG groups of 256 threads, PU tiles each
     const int tg = t >> 8;
     // the K/B stores of a batch are issued behind the next batch's loads: vmcnt counts
     // loads and stores in order, so a load issued after a store waits for it
@@ -742,6 +744,10 @@ struct LuSrc {
     const double *pop = nullptr;   // LDS populations for the residual
     double *df = nullptr;          // [N] residual out
     double *dump = nullptr;        // optional [N*N] copy of the assembled matrix (debug)
+    const double *B = nullptr;     // unfused: read the matrix from here, factor into A (NULL: A in place)
+    // unfused, boundary matrix formed from the layer's K (no electron rates): row 0 = 1,
+    // diagonal BD, above it 0.5 A_{d,r} + K_{r,d} (BE = einst), below it K_{r,d}
+    const double *BK = nullptr, *BE = nullptr, *BD = nullptr;
 };
 
 // ------------------------------------------------------------------------------
@@ -1108,13 +1114,28 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
         const int trow = (t < N) ? sm.perm[t] : 0;   // physical row of tile row t (L staging)
         if (LVG_PANEL_ONEWAVE >= 2 && t < N) sm.tmap[t] = trow;
         // ---- block column c0..c0+wJ-1 into registers (physical rows, coalesced)
-        if (!FUSED) {
+        if (!FUSED && src.BK) {
+#pragma unroll
+            for (int i = 0; i < TR; i++)
+#pragma unroll
+                for (int j = 0; j < TC; j++) {
+                    const int col = TC * cg + j, pr = prow[i], d = c0 + col;
+                    const bool ok = TR * rg + i < N && col < wJ;
+                    const double k = ok ? src.BK[(int64_t)pr * N + d] : 0.;
+                    const double e = (ok && pr < d) ? src.BE[(int64_t)d * N + pr] : 0.;
+                    const double dg = (ok && pr == d) ? src.BD[d] : 0.;
+                    double v = (pr < d) ? 0.5 * e + k : k;   // build_collision_operators: 0.5 * af + dn
+                    if (pr == d) v = dg;
+                    if (pr == 0) v = 1.;
+                    acc[i][j] = ok ? v : 0.;
+                }
+        } else if (!FUSED) {
 #pragma unroll
             for (int i = 0; i < TR; i++)
 #pragma unroll
                 for (int j = 0; j < TC; j++) {
                     const int col = TC * cg + j;
-                    acc[i][j] = (TR * rg + i < N && col < wJ) ? A[(int64_t)prow[i] * N + c0 + col] : 0.;
+                    acc[i][j] = (TR * rg + i < N && col < wJ) ? (src.B ? src.B : A)[(int64_t)prow[i] * N + c0 + col] : 0.;
                 }
         } else {
             int li[TR][TC];
@@ -1613,7 +1634,19 @@ __device__ __forceinline__ bool solve_layer(const LvgDevProblem &P, const LvgLau
     double *pops = Lc.pops + (int64_t)l * N;
     lvg_layer_status *st = reinterpret_cast<lvg_layer_status *>(Lc.status) + l;
     const bool need_boundary = (Lc.init != LVG_INIT_GIVEN);
-    build_collision_operators(P, sm, S.K, (need_boundary && !from_prev) ? S.A : nullptr);
+    // collision operator K and boundary matrix B: built here, or read from the batch
+    // built ahead by coll_kernel (K in place, B copied into the slot the LU factors in)
+    const double *Kl = S.K, *Bsrc = nullptr, *Bdg = nullptr;
+    if (Lc.kall) {
+        Kl = Lc.kall + (int64_t)l * N * N;
+        if (need_boundary && !from_prev) {
+            if (Lc.ball) Bsrc = Lc.ball + (int64_t)l * N * N;   // the boundary LU loads B from here
+            else Bdg = Lc.bdiag + (int64_t)l * N;               // ... or forms it from K
+
+        }
+    } else {
+        build_collision_operators(P, sm, S.K, (need_boundary && !from_prev) ? S.A : nullptr);
+    }
     TACC(PH_SETUP, ts0);
 
     // initial guess (radiative_transfer.cpp:247-252); the previous layer's populations
@@ -1645,9 +1678,12 @@ __device__ __forceinline__ bool solve_layer(const LvgDevProblem &P, const LvgLau
             __syncthreads();
             TACC(PH_LINES, tl0);
             TSTAMP(ta0);
-            column_diagonals(P, M, S.K, yp, sm);
+            column_diagonals(P, M, Kl, yp, sm);
             TACC(PH_ASSEMBLE, ta0);
-            src.K = S.K; src.y = yp; src.li = M.line_idx; src.pop = sm.pold; src.df = S.df;
+            src.K = Kl; src.y = yp; src.li = M.line_idx; src.pop = sm.pold; src.df = S.df;
+        } else {
+            src.B = Bsrc;
+            if (Bdg) { src.BK = Kl; src.BE = P.einst; src.BD = Bdg; }
         }
         for (int i = t; i < N; i += BT) sm.bvec[i] = (i == 0) ? 1. : 0.;
         __syncthreads();
@@ -1838,6 +1874,67 @@ __global__ void __launch_bounds__(64) lum_reduce_kernel(const LvgLumArgs *__rest
 
 #if !LVG_BIG
 #include "lvg_wave.h"
+
+// ---- collision operators of a whole batch of layers, ahead of the solve ----------------
+// build_collision_operators for every layer of the launch into K_all / B_all (HBM), with
+// a small LDS footprint (layer scalars and the rule table only) so that many workgroups
+// per CU overlap the table-fetch latency that one LU-sized workgroup per layer exposes.
+// Same function, same arithmetic: the solve reads bit-identical K and B. Any N (the
+// 16x16 pair tiles and the column sums loop over N).
+struct CollSmem {
+    double T, Te, vw, vgrad, nmol, ne;
+    double cc[LVG_MAX_COMBOS];
+    double teff[LVG_MAX_TABLES];
+    int    lo[LVG_MAX_TABLES];
+    const double *tcol[LVG_MAX_TABLES];
+    const double *tder[LVG_MAX_TABLES];
+    int64_t timax[LVG_MAX_TABLES];
+    double tdt[LVG_MAX_TABLES];
+    double tx[LVG_MAX_TABLES];
+    int8_t ttab[LVG_MAX_CLASSES][LVG_MAX_TERMS], tcombo[LVG_MAX_CLASSES][LVG_MAX_TERMS];
+    int8_t tet[LVG_MAX_CLASSES], tgrp[LVG_MAX_CLASSES];
+    double dust[LVG_MAX_DUST];
+    union { double d[1]; } pu;          // too small to stage pair classes: they come from HBM
+};
+
+#ifndef LVG_COLL_K_PU
+#define LVG_COLL_K_PU 2               // pair tiles per batch in coll_kernel (1 and 8 WG/CU variants spill)
+#endif
+#ifndef LVG_COLL_K_OCC
+#define LVG_COLL_K_OCC 4              // workgroups per CU coll_kernel is built for (register budget)
+#endif
+__global__ void __launch_bounds__(BT, LVG_COLL_K_OCC) coll_kernel(const LvgDevProblem *__restrict__ Pp,
+                                                                  const LvgLaunch *__restrict__ Lp) {
+    __shared__ CollSmem sm;
+    const LvgDevProblem &P = *Pp;
+    const LvgLaunch &Lc = *Lp;
+    PH_INIT();
+    load_rule_table(P, sm);
+    const int64_t NN = (int64_t)P.N * P.N;
+    for (int l = blockIdx.x; l < Lc.nb_lay; l += gridDim.x) {
+        if (threadIdx.x == 0) layer_scalars(P, Lc, l, sm);
+        __syncthreads();
+        double *Kl = const_cast<double *>(Lc.kall) + l * NN;
+        build_collision_operators<CollSmem, LVG_COLL_K_PU>(P, sm, Kl, Lc.ball ? const_cast<double *>(Lc.ball) + l * NN : nullptr);
+        if (Lc.bdiag) {
+            // B's diagonal only (no electron rates: B = K + A/2 above the diagonal, K below):
+            // minus the ascending column sum, as build_collision_operators forms it
+            const int N = P.N;
+            for (int d = threadIdx.x; d < N; d += BT) {
+                double a = 0.;
+                for (int r = 0; r < N; r++) {
+                    if (r == d) continue;
+                    const double k = Kl[(int64_t)r * N + d];
+                    const double b = (r < d) ? 0.5 * P.einst[(int64_t)d * N + r] + k : k;
+                    a = a - b;
+                }
+                const_cast<double *>(Lc.bdiag)[(int64_t)l * N + d] = a;
+            }
+        }
+        __syncthreads();
+    }
+    PH_FLUSH();
+}
 #endif
 
 }  // namespace LVG_NS
@@ -1855,6 +1952,13 @@ extern "C" hipError_t LVG_SYM(lvg_launch_solve)(const LvgDevProblem *P, const Lv
     hipLaunchKernelGGL(LVG_NS::solve_kernel, dim3(grid), dim3(LVG_NS::BT), 0, s, P, L);
     return hipGetLastError();
 }
+
+#if !LVG_BIG
+extern "C" hipError_t lvg_launch_coll(const LvgDevProblem *P, const LvgLaunch *L, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(lvg::coll_kernel, dim3(grid), dim3(lvg::BT), 0, s, P, L);
+    return hipGetLastError();
+}
+#endif
 
 extern "C" hipError_t LVG_SYM(lvg_launch_debug)(const LvgDevProblem *P, const LvgLaunch *L, hipStream_t s) {
     hipLaunchKernelGGL(LVG_NS::debug_kernel, dim3(1), dim3(LVG_NS::BT), 0, s, P, L);

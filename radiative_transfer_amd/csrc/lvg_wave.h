@@ -555,6 +555,9 @@ __device__ __forceinline__ void wave_line_terms_overlap(const LvgDevProblem &P, 
 // oracle's (physically swapped) row order, tracked here as each row's logical
 // position lp; every a_ij receives fma(-l_ik, u_kj, a_ij) for k ascending; x_k =
 // b_k / u_kk and b_i = fma(-u_ik, x_k, b_i) for k descending.
+#ifndef LVG_WAVE_LOOKAHEAD
+#define LVG_WAVE_LOOKAHEAD 1          // next column's pivot reduction overlapped with this column's update
+#endif
 #ifndef LVG_WAVE_LDS_BCAST
 #define LVG_WAVE_LDS_BCAST 0          // 1: pivot row broadcast through LDS (measured slower than v_readlane)
 #endif
@@ -564,6 +567,55 @@ __device__ __forceinline__ void wave_lu_solve(double (&a)[NM], double rb, int N,
     TSTAMP(tf0);
     bool act = ln < N;
     int lp = ln;
+#if LVG_WAVE_LOOKAHEAD
+    // Look-ahead pivot search: column c+1 is updated first and its max-key reduction (a
+    // dependent DPP chain) is issued before the rest of column c's row update, so the two
+    // overlap. Same pivots and the same fma per element as the plain loop below.
+    unsigned khi, klo, H;
+    auto col_key = [&](int c, double v) {
+        const double av = fabs(v);
+        const unsigned long long bits = (act && av == av) ? (unsigned long long)__double_as_longlong(av) : 0ull;
+        const bool dnan = act && lp == c && av != av;
+        khi = dnan ? 0xffffffffu : act ? ((unsigned)(bits >> 32) | 0x80000000u) : 0u;
+        klo = dnan ? 0xffffffffu : (unsigned)bits;
+    };
+    col_key(0, a[0]);
+    H = wave_max_u32(khi);
+#pragma unroll
+    for (int c = 0; c < NM; c++) {
+        if (c < N) {
+            const unsigned long long tie = __ballot(khi == H);
+            int pl;
+            if (__popcll(tie) == 1) {
+                pl = __ffsll((long long)tie) - 1;
+            } else {
+                const unsigned Lw = wave_max_u32(khi == H ? klo : 0u);
+                const unsigned X = wave_max_u32((khi == H && klo == Lw && act) ? ~(unsigned)lp : 0u);
+                const int wmin = (int)~X;
+                pl = __ffsll((long long)__ballot(act && khi == H && klo == Lw && lp == wmin)) - 1;
+            }
+            pl = __builtin_amdgcn_readfirstlane(pl);
+            const int plp = __builtin_amdgcn_readlane(lp, pl);
+            const double piv = readlane_d(a[c], pl);
+            const double bc = readlane_d(rb, pl);
+            if (ln == pl) { act = false; lp = c; }
+            else if (lp == c) lp = plp;
+            const double l = a[c] / piv;
+            if (c + 1 < NM) {
+                const double u = readlane_d(a[c + 1], pl);
+                a[c + 1] = act ? fma(-l, u, a[c + 1]) : a[c + 1];
+                col_key(c + 1, a[c + 1]);
+                H = wave_max_u32(khi);
+            }
+#pragma unroll
+            for (int j = c + 2; j < NM; j++) {
+                const double u = readlane_d(a[j], pl);
+                a[j] = act ? fma(-l, u, a[j]) : a[j];
+            }
+            if (act) { a[c] = l; rb = fma(-l, bc, rb); }
+        }
+    }
+#else
 #pragma unroll
     for (int c = 0; c < NM; c++) {
         if (c < N) {
@@ -632,6 +684,7 @@ __device__ __forceinline__ void wave_lu_solve(double (&a)[NM], double rb, int N,
             }
         }
     }
+#endif
     TACC(PH_PANEL, tf0);
     TSTAMP(tb0);
 #pragma unroll
