@@ -243,6 +243,7 @@ def main():
     if rank == 0:
         value = units_total * args.steps / elapsed
         kms = float(np.mean(kern_ms))
+        ms_step = 1e3 * elapsed / args.steps
         kernel = "lvg::solve_wave_kernel" if N <= 64 else "lvg::solve_kernel" if N <= 256 else "lvg_big::solve_kernel"
         bound = binding_roof(N)
         per_launch = units_local
@@ -263,6 +264,10 @@ def main():
                      # collision operators of the batch, built ahead by lvg::coll_kernel (in the
                      # step time, not in kernel_ms; 0 when each layer builds its own in-kernel)
                      "coll_kernel_ms": float(np.mean(coll_ms)),
+                     # the same flops over the whole step (collision build, queue sort and the
+                     # status reduction included)
+                     "fp64_frac_step": flops_per_layer_iteration(N) * per_launch / (ms_step * 1e-3) / 1e12
+                     / PEAK_FP64_TFLOPS,
                      "flops_per_unit": flops_per_layer_iteration(N),
                      "hbm_model_bytes_per_unit": bytes_per_layer_iteration(N), "units_per_launch": per_launch,
                      "fp64_frac": flops_per_layer_iteration(N) * per_launch / (kms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS,
