@@ -26,6 +26,8 @@
 
 extern "C" hipError_t lvg_launch_solve(const LvgDevProblem *P, const LvgLaunch *L, int grid, hipStream_t s);
 extern "C" hipError_t lvg_launch_coll(const LvgDevProblem *P, const LvgLaunch *L, int grid, hipStream_t s);
+extern "C" hipError_t lvg_row_order(const double *soa, int ld, int n, int row, double *keys, double *keys_sorted,
+                                    int *idx, int *order, void *temp, size_t *temp_bytes, hipStream_t s);
 extern "C" int lvg_wave_plan(int N, int nb_y, int grid_doubles, size_t lds_cap, int *wpb, size_t *dyn);
 extern "C" hipError_t lvg_wave_occupancy(int N, int wpb, size_t dyn, int *blocks_per_cu);
 extern "C" hipError_t lvg_launch_solve_wave(const LvgDevProblem *P, const LvgLaunch *L, int N, int grid, int wpb,
@@ -90,6 +92,8 @@ struct lvg_handle {
     size_t sched_cap = 0, sched_tmp_cap = 0;
     void *d_coll = nullptr;            // K_all, B_all of the last coll_kernel batch
     size_t coll_cap = 0;
+    void *d_corder = nullptr;          // coll_kernel temperature order + its sort scratch
+    size_t corder_cap = 0;
     // warm chains: offsets [nb_chain + 1] then queue order [nb_chain] (device + host staging)
     int *d_chain = nullptr;
     size_t chain_cap = 0;
@@ -685,6 +689,7 @@ void lvg_destroy(lvg_handle *h) {
     if (h->d_sched) (void)hipFree(h->d_sched);
     if (h->d_sched_tmp) (void)hipFree(h->d_sched_tmp);
     if (h->d_coll) (void)hipFree(h->d_coll);
+    if (h->d_corder) (void)hipFree(h->d_corder);
     if (h->d_chain) (void)hipFree(h->d_chain);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -853,6 +858,20 @@ int launch_solve(lvg_handle *h, int nb_lay, const double *d_soa, double *d_pops,
             L.ball = (need_b && !b_from_k) ? tail : nullptr;
             L.bdiag = (need_b && b_from_k) ? tail : nullptr;
             coll_ahead = true;
+            if (!std::getenv("LVG_COLL_INDEX_ORDER")) {
+                // temperature order for coll_kernel (lvg_sched.hip); its own scratch, since
+                // the solve queue's order may live in d_sched
+                size_t tmp = 0;
+                HIPCHECK(h, lvg_row_order(nullptr, nb_lay, nb_lay, 0, nullptr, nullptr, nullptr, nullptr, nullptr, &tmp, s));
+                if ((rc = grow(h, &h->d_corder, &h->corder_cap,
+                               (size_t)nb_lay * (2 * sizeof(double) + 2 * sizeof(int)) + tmp + 256))) return rc;
+                double *keys = static_cast<double *>(h->d_corder), *keys2 = keys + nb_lay;
+                int *idx = reinterpret_cast<int *>(keys2 + nb_lay), *ord = idx + nb_lay;
+                char *scratch = reinterpret_cast<char *>(ord + nb_lay);
+                scratch += (256 - (reinterpret_cast<uintptr_t>(scratch) & 255)) & 255;
+                HIPCHECK(h, lvg_row_order(d_soa, nb_lay, nb_lay, 0, keys, keys2, idx, ord, scratch, &tmp, s));
+                L.coll_order = ord;
+            }
         }
     }
     const LvgLaunch *dL = nullptr;

@@ -102,6 +102,7 @@ struct LvgLaunch {
     // without electron tables B is K + A/2 above the diagonal and K below it: then only
     // its diagonal is stored, bdiag [nb_lay][N], and the boundary LU forms B from K
     const double *bdiag;
+    const int *coll_order;            // coll_kernel: position -> layer (temperature order), NULL: index order
     // debug probe outputs (lvg_debug_calc_new_pop)
     double   *dbg_matrix, *dbg_df, *dbg_pop_in;
     int       dbg_mode;               // 0 solve, 1 debug calc_new_pop, 2 boundary pops only

@@ -1911,7 +1911,13 @@ __global__ void __launch_bounds__(BT, LVG_COLL_K_OCC) coll_kernel(const LvgDevPr
     PH_INIT();
     load_rule_table(P, sm);
     const int64_t NN = (int64_t)P.N * P.N;
-    for (int l = blockIdx.x; l < Lc.nb_lay; l += gridDim.x) {
+    // XCD-aware: workgroups are dispatched round-robin over the 8 XCDs, so workgroup b
+    // takes position chunk (b % 8) of the temperature-ordered list: each XCD's resident
+    // layers span a narrow temperature range and share table rows in its L2
+    const int G = gridDim.x, b = blockIdx.x;
+    const int rb = (G % 8 == 0) ? (b % 8) * (G / 8) + b / 8 : b;
+    for (int pos = rb; pos < Lc.nb_lay; pos += G) {
+        const int l = Lc.coll_order ? Lc.coll_order[pos] : pos;
         if (threadIdx.x == 0) layer_scalars(P, Lc, l, sm);
         __syncthreads();
         double *Kl = const_cast<double *>(Lc.kall) + l * NN;
