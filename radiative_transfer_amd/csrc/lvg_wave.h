@@ -28,6 +28,9 @@
 #ifndef LVG_WAVE_LINE_INV
 #define LVG_WAVE_LINE_INV 1           // line terms from per-layer invariant records (wave_line_invariants)
 #endif
+#ifndef LVG_WAVE_KROW
+#define LVG_WAVE_KROW 1               // 1: the lane's K / line-index row held in registers for the layer
+#endif
 #ifndef LVG_WAVE_ACCEL_BATCH
 #define LVG_WAVE_ACCEL_BATCH 1        // Ng sums: ring reads of 8 levels per round trip
 #endif
@@ -904,6 +907,17 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
     bool boundary = need_boundary && !from_prev, found = false;
     int iters = 0, retry = 0;
     const int row = t < N ? t : 0;
+#if LVG_WAVE_KROW
+    // the lane's row of K and of the line-index map, fixed for the layer, in registers
+    double krow[NM];
+    int lrow[NM];
+#pragma unroll
+    for (int j = 0; j < NM; j++) {
+        const int jj = (j < N) ? j : 0;
+        krow[j] = K[row * ldk + jj];
+        lrow[j] = (j < N) ? li[row * ldk + jj] : -1;
+    }
+#endif
     if (!boundary) wave_start_pass(C, S, Lc, N, accel ? Lc.max_iter_acc : Lc.max_iter_plain, accel);
     for (;;) {
         double a[NM];
@@ -979,7 +993,13 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
                     const int j = j0 + u;
-                    if (LVG_WAVE_CLAMP) {
+                    if (LVG_WAVE_KROW) {
+#if LVG_WAVE_KROW
+                        kc[u] = krow[j];
+                        lc[u] = lrow[j];
+                        pc[u] = sm.pold[j];
+#endif
+                    } else if (LVG_WAVE_CLAMP) {
                         const int jj = (j < N) ? j : 0;
                         kc[u] = K[row * ldk + jj];
                         const int lv = li[row * ldk + jj];
