@@ -1,15 +1,22 @@
 #!/usr/bin/env python3
 """Benchmark: layer-iterations/s of the LVG level-population solve (BASELINE.json metric).
 
-Default workload: CH3OH-A, 256 levels, ONE 4096-layer cloud (BASELINE.json configs[2]),
-layer-sharded over the ranks with dist.shard_range — strong scaling: `--gpus N` splits
-the same 4096 layers N ways (`--weak` keeps 4096 layers per GPU instead).
-`--workload` selects the other BASELINE configs for their own lines: ph2o45_1024
-(configs[1]), ch3ohe256_sweep (configs[3], 128x128 = 16384 cells), oh24_overlap_2048
-(configs[4]). `--chain-len C` switches to the reference's default start rule
-(LVG_INIT_WARM_CHAIN, radiative_transfer.cpp:247-252): the rank's layers become
-independent clouds of C consecutive layers, each a warm chain, all solved in one
-launch (lvg_solve_chains_device; one workgroup / wave per chain).
+Default workload: CH3OH-A, 256 levels, 4096 layers per GPU (BASELINE.json configs[2]),
+layer-sharded over the ranks with dist.shard_range — weak scaling: with `--gpus N` the
+cloud has 4096·N layers (synth_v1) and every rank solves its contiguous block of 4096;
+`--strong` splits one 4096-layer cloud N ways instead. `--workload` selects the other
+BASELINE configs for their own lines: ph2o45_1024 (configs[1]), ch3ohe256_sweep
+(configs[3], 128x128 = 16384 cells), oh24_overlap_2048 (configs[4]). `--chain-len C`
+switches to the reference's default start rule (LVG_INIT_WARM_CHAIN,
+radiative_transfer.cpp:247-252): the rank's layers become independent clouds of C
+consecutive layers, each a warm chain, all solved in one launch (lvg_solve_chains_device;
+one workgroup / wave per chain).
+
+Launch. `python bench.py --gpus N` starts N rank processes itself (one per GPU, before
+this process touches a GPU) with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
+MASTER_PORT set, waits for them and exits with the first failure's code; rank 0 prints
+the line. Under torchrun (WORLD_SIZE already set) this process is one rank. `--gpus N`
+with fewer than N visible GPUs fails before anything starts.
 
 A "step" is one full batched solve of this rank's layers: per layer the collision
 operator, boundary_layer_populations, and the iteration_control loop (calc_new_pop =
@@ -31,6 +38,7 @@ import argparse
 import json
 import os
 import platform
+import socket
 import subprocess
 import sys
 import time
@@ -44,6 +52,7 @@ METRIC = "layer-iterations/sec, CH3OH-A 256 lev × 4096 layers, 1/2/4/8 GPU"
 UNIT = "layer-iterations/s"
 PEAK_FP64_TFLOPS = 78.6      # MI355X FP64 peak (vector and matrix alike), spec
 PEAK_HBM_GBS = 8000.0        # MI355X HBM3E, spec
+CLOCK_GHZ = 2.4              # MI355X max engine clock (MI355X_MICROARCH.md)
 
 
 def flops_per_layer_iteration(N: int) -> float:
@@ -63,6 +72,14 @@ def binding_roof(N: int) -> str:
     return "hbm" if hbm < fp64 else "fp64"
 
 
+def latency_floor_cycles(N: int) -> float:
+    """Dependent-chain floor of one calc_new_pop on one wave: the LU's N
+    pivot columns are sequential, and each needs at least a 7-step DPP max reduction, a
+    readlane broadcast and an fp64 division before the next column's key exists —
+    about 10 dependent vector operations at >= 8 cycles each."""
+    return 80.0 * N
+
+
 def load_pmc_traffic(workload: str):
     """HBM bytes per launch from a committed rocprofv3 --pmc pass (not measured in this run)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -72,7 +89,7 @@ def load_pmc_traffic(workload: str):
         if not e:
             return None, None
         return float(e["hbm_bytes_per_launch"]), f"{e.get('source', p)} ({e.get('round', '?')}, " \
-            f"{e.get('units_per_launch', '?')} units/launch)"
+            f"{e.get('units_per_launch', '?')} units/launch, commit {e.get('commit', '?')})"
     except Exception:
         return None, None
 
@@ -94,6 +111,72 @@ def host_info() -> dict:
         pass
     return info
 
+
+# ---- GPU provenance (clock, power, identity), read by a child process ------------------
+
+_SMI = ["rocm-smi", "--showclocks", "--showpower", "--showuniqueid", "--showserial", "--showproductname", "--json"]
+
+
+def _smi_start():
+    try:
+        return subprocess.Popen(_SMI, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+    except Exception:
+        return None
+
+
+def _smi_finish(p) -> dict:
+    """Per card: sclk, mclk, socket power, unique id / serial, product (rocm-smi --json)."""
+    if p is None:
+        return {"error": "rocm-smi not runnable"}
+    try:
+        out, _ = p.communicate(timeout=30)
+        raw = json.loads(out)
+    except Exception as e:           # noqa: BLE001 - provenance is best effort, never fatal
+        try:
+            p.kill()
+        except Exception:
+            pass
+        return {"error": f"rocm-smi: {type(e).__name__}"}
+    cards = {}
+    for card, d in raw.items():
+        if not isinstance(d, dict):
+            continue
+        pick = {}
+        for k, v in d.items():
+            kl = k.lower()
+            if ("sclk" in kl or "mclk" in kl) and "clock level" in kl:
+                pick[k.split("(")[0].strip()] = v
+            elif "power" in kl and "(w)" in kl:
+                pick["power_w"] = v
+            elif "unique id" in kl or "serial" in kl or kl.startswith("card series") or kl.startswith("card sku"):
+                pick[k] = v
+        cards[card] = pick
+    return cards
+
+
+class Provenance:
+    """rocm-smi before the timed region (GPU idle), one started as the timed region
+    begins (its sample lands inside it when the region outlasts the query), and one after."""
+
+    def __init__(self, enabled: bool):
+        self.enabled = enabled
+        self.rec = {"host": socket.gethostname(), "hip_visible_devices": os.environ.get("HIP_VISIBLE_DEVICES")}
+        if enabled:
+            self.rec["before"] = _smi_finish(_smi_start())
+        self._during = None
+
+    def timed_start(self):
+        if self.enabled:
+            self._during = _smi_start()
+
+    def timed_end(self):
+        if self.enabled:
+            self.rec["during"] = _smi_finish(self._during)
+            self.rec["after"] = _smi_finish(_smi_start())
+        return self.rec
+
+
+# ---- CPU baseline (the oracle: test infrastructure, timed beside the GPU) ---------------
 
 def cpu_leg(prob, layers, opts, budget_s: float, threads: int, chain_len: int = 0):
     """Oracle (C restatement, OpenMP schedule(dynamic,1) over layers, or over clouds for
@@ -137,46 +220,114 @@ def cpu_baseline(prob, layers, opts, budget_s: float, chain_len: int = 0):
             "host": info}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="ch3oha256_4096")
-    ap.add_argument("--layers", type=int, default=0, help="cloud layers (default: the config's)")
-    ap.add_argument("--nb-lev", type=int, default=0, help="levels (default: the config's; 768 = reference CH3OH)")
-    ap.add_argument("--weak", action="store_true", help="config's layers PER GPU instead of one cloud")
-    ap.add_argument("--chain-len", type=int, default=0,
-                    help="warm chains of this many layers (LVG_INIT_WARM_CHAIN) instead of independent layers")
-    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds per CPU leg")
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-host-entry", action="store_true")
-    args = ap.parse_args()
+# ---- launcher -----------------------------------------------------------------------------
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def visible_gpus() -> int:
+    """GPUs this process could use (torch.cuda.device_count() does not initialise the GPU
+    on this image, so the launcher can ask before it starts the ranks)."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def launch_ranks(args, argv) -> int:
+    """One child per rank, each `bench.py <same args>` with the torch.distributed env."""
+    n = args.gpus
+    if not args.stub:
+        have = visible_gpus()
+        if have < n:
+            print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have}", file=sys.stderr)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in live:          # a rank failed: the others would wait at a barrier
+                    q.kill()
+    return rc if rc >= 0 else 128 - rc
+
+
+# ---- one rank -----------------------------------------------------------------------------
+
+class StubSolver:
+    """CPU stand-in for the launcher test (--stub): no GPU, no oracle; every layer reports
+    3 iterations. Exercises the rank setup, sharding, status reduction and reporting."""
+    N = 0
+
+    def __init__(self, N):
+        self.N = N
+
+    def solve_layers_device(self, n, soa, pops, status, opts, stream_ptr=0):
+        pass
+
+    def solve_chains_device(self, n, soa, offs, pops, status, opts, stream_ptr=0):
+        pass
+
+    def last_kernel_time(self):
+        return 1.0, 1
+
+    def last_coll_time(self):
+        return 0.0
+
+    def close(self):
+        pass
+
+
+def run_rank(args) -> int:
     import torch
     from radiative_transfer_amd import abi, dist, synth
-    from radiative_transfer_amd.native import LvgSolver
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    gpus = args.gpus if args.gpus is not None else world
+    if gpus != world:
+        print(f"bench.py: --gpus {gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        return 2
     multi = world > 1
+    stub = args.stub
     if multi:
         import torch.distributed as td
-        torch.cuda.set_device(local)
-        td.init_process_group(backend="nccl")
-    else:
+        if not stub:
+            torch.cuda.set_device(local)
+        td.init_process_group(backend="gloo" if stub else "nccl")
+    elif not stub:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
+    dev = torch.device("cpu") if stub else torch.device("cuda", torch.cuda.current_device())
+
+    def sync():
+        if not stub:
+            torch.cuda.synchronize()
 
     kind, N, L_cfg, seed = synth.CONFIGS[args.workload]
     N = args.nb_lev or N
     L_cloud = args.layers or L_cfg
-    total = L_cloud * world if args.weak else L_cloud
+    total = L_cloud if args.strong else L_cloud * world
     prob, layers_all, o = synth.make_problem(args.workload, nb_lay=total, nb_lev=N)
     opts = abi.default_opts(**o)
     if args.chain_len:
         opts.init = abi.LVG_INIT_WARM_CHAIN
+    offs_all = c_lo = c_hi = None
     if args.chain_len:
         # clouds of chain_len consecutive layers; whole clouds per rank (dist.chain_shard)
         offs_all = chain_offsets(total, args.chain_len)
@@ -187,31 +338,44 @@ def main():
     mine = layers_all.subset(np.arange(lo, hi))
     n_mine = hi - lo
 
-    solver = LvgSolver(prob, device=dev.index)
+    if stub:
+        solver = StubSolver(N)
+    else:
+        from radiative_transfer_amd.native import LvgSolver
+        solver = LvgSolver(prob, device=dev.index)
+        if args.tuning:
+            solver.set_tuning(args.tuning)
     soa = torch.from_numpy(mine.soa()).to(dev)
     pops = torch.zeros((max(n_mine, 1), N), dtype=torch.float64, device=dev)
     status = torch.zeros((max(n_mine, 1), abi.STATUS_DTYPE.itemsize // 8), dtype=torch.float64, device=dev)
-    stream = torch.cuda.current_stream(dev)
-
+    if stub:
+        status.view(torch.int32)[:, abi.STATUS_DTYPE.fields["iterations"][1] // 4] = 3
+        status.view(torch.int32)[:, abi.STATUS_DTYPE.fields["converged"][1] // 4] = 1
+    stream_ptr = 0 if stub else torch.cuda.current_stream(dev).cuda_stream
     offs = (offs_all[c_lo:c_hi + 1] - lo).astype(np.int32) if args.chain_len else None
 
     def step():
-        if offs is not None:
-            solver.solve_chains_device(n_mine, soa.data_ptr(), offs, pops.data_ptr(), status.data_ptr(), opts,
-                                       stream_ptr=stream.cuda_stream)
-        else:
-            solver.solve_layers_device(n_mine, soa.data_ptr(), pops.data_ptr(), status.data_ptr(), opts,
-                                       stream_ptr=stream.cuda_stream)
+        if n_mine > 0:                          # a rank may hold no clouds / layers at all
+            if offs is not None:
+                solver.solve_chains_device(n_mine, soa.data_ptr(), offs, pops.data_ptr(), status.data_ptr(), opts,
+                                           stream_ptr=stream_ptr)
+            else:
+                solver.solve_layers_device(n_mine, soa.data_ptr(), pops.data_ptr(), status.data_ptr(), opts,
+                                           stream_ptr=stream_ptr)
         return dist.reduce_status_device(status[:n_mine])
 
     for _ in range(max(1, args.warmup)):
         step()
-    torch.cuda.synchronize()
-    units_local = int(dist.status_numpy(status[:n_mine])["iterations"].sum())
+    sync()
+    st1 = dist.status_numpy(status[:n_mine])
+    units_local = int(st1["iterations"].sum())
+    max_layer_its = int(st1["iterations"].max()) if n_mine else 0
 
+    prov = Provenance(enabled=(rank == 0 and not stub and not args.no_provenance))
     if multi:
         td.barrier()
-    torch.cuda.synchronize()
+    sync()
+    prov.timed_start()
     kern_ms, coll_ms = [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -219,20 +383,24 @@ def main():
         ms, _ = solver.last_kernel_time()
         kern_ms.append(ms)
         coll_ms.append(solver.last_coll_time())
-    torch.cuda.synchronize()
+    sync()
     if multi:
         td.barrier()
     elapsed = time.perf_counter() - t0
+    prov_rec = prov.timed_end()
     st2 = dist.status_numpy(status[:n_mine])
     assert int(st2["iterations"].sum()) == units_local, "iteration count changed between steps"
     if multi:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         td.all_reduce(tt, op=td.ReduceOp.MAX)
         elapsed = float(tt.item())
+        ml = torch.tensor([float(max_layer_its)], dtype=torch.float64, device=dev)
+        td.all_reduce(ml, op=td.ReduceOp.MAX)
+        max_layer_its = int(ml.item())
     units_total, nonconv, max_rel = int(glob[0].item()), int(glob[1].item()), float(glob[2].item())
 
     host_value = None
-    if rank == 0 and world == 1 and not args.no_host_entry:
+    if rank == 0 and world == 1 and not args.no_host_entry and not stub:
         th = time.perf_counter()
         if offs is not None:
             _, sh = solver.solve_chains(mine, offs, opts)
@@ -241,62 +409,109 @@ def main():
         host_value = int(sh["iterations"].sum()) / (time.perf_counter() - th)
 
     if rank == 0:
-        value = units_total * args.steps / elapsed
-        kms = float(np.mean(kern_ms))
-        ms_step = 1e3 * elapsed / args.steps
-        kernel = "lvg::solve_wave_kernel" if N <= 64 else "lvg::solve_kernel" if N <= 256 else "lvg_big::solve_kernel"
-        bound = binding_roof(N)
-        per_launch = units_local
-        # committed PMC traffic applies only to the profiled configuration
-        traffic, tsrc = load_pmc_traffic(args.workload) if (N, total) == (synth.CONFIGS[args.workload][1],
-                                                                           L_cfg) and not args.chain_len else (None, None)
-        if bound == "fp64":
-            achieved = flops_per_layer_iteration(N) * per_launch / (kms * 1e-3) / 1e12
-            roof = {"bound": "fp64", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                    "frac": achieved / PEAK_FP64_TFLOPS,
-                    "peak_note": "MI355X FP64 peak 78.6 TF/s (vector FMA and v_mfma_f64 alike; not an MFMA claim)"}
-        else:
-            achieved = bytes_per_layer_iteration(N) * per_launch / (kms * 1e-3) / 1e9
-            roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": achieved / PEAK_HBM_GBS}
-        roof.update({"traffic": traffic, "traffic_source": tsrc if traffic else None,
-                     "kernel": kernel, "kernel_ms": kms,
-                     # collision operators of the batch, built ahead by lvg::coll_kernel (in the
-                     # step time, not in kernel_ms; 0 when each layer builds its own in-kernel)
-                     "coll_kernel_ms": float(np.mean(coll_ms)),
-                     # the same flops over the whole step (collision build, queue sort and the
-                     # status reduction included)
-                     "fp64_frac_step": flops_per_layer_iteration(N) * per_launch / (ms_step * 1e-3) / 1e12
-                     / PEAK_FP64_TFLOPS,
-                     "flops_per_unit": flops_per_layer_iteration(N),
-                     "hbm_model_bytes_per_unit": bytes_per_layer_iteration(N), "units_per_launch": per_launch,
-                     "fp64_frac": flops_per_layer_iteration(N) * per_launch / (kms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS,
-                     "hbm_model_frac": bytes_per_layer_iteration(N) * per_launch / (kms * 1e-3) / 1e9 / PEAK_HBM_GBS})
-        out = {
-            "metric": METRIC, "value": value, "unit": UNIT, "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,
-            "scaling": "weak" if args.weak else "strong", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (synth_v1, SURVEY.md 8d)",
-            "config": {"workload": args.workload, "nb_lev": N, "layers_total": total,
-                       "layers_per_gpu": hi - lo if world == 1 else f"{total // world}-{-(-total // world)}",
-                       "layer_iterations_per_step": units_total, "nonconverged_layers": nonconv,
-                       "max_rel_error": max_rel,
-                       "parallelism": f"clouds sharded x{world} (dist.chain_shard)" if args.chain_len
-                       else f"layers sharded x{world} (dist.shard_range)",
-                       "init": f"warm_chain x{len(offs) - 1} clouds of {args.chain_len} layers" if offs is not None
-                       else "boundary_layer", "acceleration": bool(opts.acceleration),
-                       "line_overlap": bool(opts.line_overlap)},
-            "roofline": roof,
-        }
-        if host_value is not None:
-            out["host_entry_value"] = host_value
-        if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(prob, mine, opts, args.cpu_budget, args.chain_len)
-        print(json.dumps(out))
+        print(json.dumps(report(args, world, N, total, L_cfg, lo, hi, units_total, units_local, nonconv, max_rel,
+                                max_layer_its, elapsed, kern_ms, coll_ms, opts, offs, prov_rec, host_value,
+                                prob, mine, stub)), flush=True)
     solver.close()
     if multi:
         td.destroy_process_group()
+    return 0
+
+
+def report(args, world, N, total, L_cfg, lo, hi, units_total, units_local, nonconv, max_rel, max_layer_its,
+           elapsed, kern_ms, coll_ms, opts, offs, prov_rec, host_value, prob, mine, stub):
+    from radiative_transfer_amd import synth
+    value = units_total * args.steps / elapsed
+    kms = float(np.mean(kern_ms))
+    cms = float(np.mean(coll_ms))
+    ms_step = 1e3 * elapsed / args.steps
+    kernel = "lvg::solve_wave_kernel" if N <= 64 else "lvg::solve_kernel" if N <= 256 else "lvg_big::solve_kernel"
+    bound = binding_roof(N)
+    per_launch = units_local
+    F, B = flops_per_layer_iteration(N), bytes_per_layer_iteration(N)
+    # committed PMC traffic applies only to the profiled configuration
+    profiled = (N, hi - lo) == (synth.CONFIGS[args.workload][1], L_cfg) and not args.chain_len and not args.tuning
+    traffic, tsrc = load_pmc_traffic(args.workload) if profiled else (None, None)
+    if bound == "fp64":
+        achieved = F * per_launch / (kms * 1e-3) / 1e12
+        roof = {"bound": "fp64", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / PEAK_FP64_TFLOPS,
+                "peak_note": "MI355X FP64 peak 78.6 TF/s (vector FMA and v_mfma_f64 alike; not an MFMA claim)"}
+    else:
+        achieved = B * per_launch / (kms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": achieved / PEAK_HBM_GBS}
+    roof.update({"traffic": traffic, "traffic_source": tsrc if traffic else None,
+                 "kernel": kernel, "kernel_ms": kms,
+                 # collision operators of the batch built ahead by lvg::coll_kernel (0 unless
+                 # the tuning turns it on; not in kernel_ms)
+                 "coll_kernel_ms": cms,
+                 # the same flops over the whole step (queue sort, any collision pre-build and
+                 # the status reduction included): the headline FP64 fraction
+                 "fp64_frac_step": F * per_launch / (ms_step * 1e-3) / 1e12 / PEAK_FP64_TFLOPS,
+                 "flops_per_unit": F, "hbm_model_bytes_per_unit": B, "units_per_launch": per_launch,
+                 "fp64_frac": F * per_launch / (kms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS,
+                 "hbm_model_frac": B * per_launch / (kms * 1e-3) / 1e9 / PEAK_HBM_GBS})
+    # When every layer of the launch is resident at once (the small-N configs), the launch
+    # lasts as long as its slowest layer: a latency bound, stated against a chain floor.
+    slowest = max_layer_its + 1                     # + the boundary-layer LU
+    us_it = kms * 1e3 / slowest if slowest else 0.
+    floor = latency_floor_cycles(N)
+    roof["latency"] = {"slowest_layer_iterations": max_layer_its, "us_per_slowest_layer_iteration": us_it,
+                       "cycles_per_iteration_at_2.4GHz": us_it * 1e-6 * CLOCK_GHZ * 1e9,
+                       "floor_cycles_per_iteration": floor,
+                       "floor_model": "N pivot columns x 80 cycles (7-step DPP max, readlane, fp64 division)",
+                       "frac": floor / (us_it * 1e-6 * CLOCK_GHZ * 1e9) if us_it else None,
+                       "binds": N <= 64}
+    layers_rank = hi - lo
+    out = {
+        "metric": METRIC, "value": value, "unit": UNIT, "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
+        "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (synth_v1, SURVEY.md 8d)" + (" [STUB solver: launcher test]" if stub else ""),
+        "config": {"workload": args.workload, "nb_lev": N, "layers_total": total,
+                   "layers_per_gpu": layers_rank if world == 1 or not args.strong
+                   else f"{total // world}-{-(-total // world)}",
+                   "layer_iterations_per_step": units_total, "nonconverged_layers": nonconv,
+                   "max_rel_error": max_rel,
+                   "parallelism": f"clouds sharded x{world} (dist.chain_shard)" if args.chain_len
+                   else f"layers sharded x{world} (dist.shard_range)",
+                   "init": f"warm_chain x{len(offs) - 1} clouds of {args.chain_len} layers" if offs is not None
+                   else "boundary_layer", "acceleration": bool(opts.acceleration),
+                   "line_overlap": bool(opts.line_overlap), "tuning": args.tuning or None},
+        "roofline": roof,
+        "provenance": prov_rec,
+    }
+    if host_value is not None:
+        out["host_entry_value"] = host_value
+    if world == 1 and not args.no_cpu and not stub:
+        out["cpu_baseline"] = cpu_baseline(prob, mine, opts, args.cpu_budget, args.chain_len)
+    return out
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (one per GPU); default 1, or WORLD_SIZE")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="ch3oha256_4096")
+    ap.add_argument("--layers", type=int, default=0, help="layers per GPU (--strong: of the cloud); default the config's")
+    ap.add_argument("--nb-lev", type=int, default=0, help="levels (default: the config's; 768 = reference CH3OH)")
+    ap.add_argument("--strong", action="store_true", help="split ONE cloud of the config's layers over the GPUs")
+    ap.add_argument("--chain-len", type=int, default=0,
+                    help="warm chains of this many layers (LVG_INIT_WARM_CHAIN) instead of independent layers")
+    ap.add_argument("--tuning", default="", help="lvg_set_tuning spec (diagnostics; results unchanged)")
+    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds per CPU leg")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-host-entry", action="store_true")
+    ap.add_argument("--no-provenance", action="store_true")
+    ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)   # launcher test, CPU only
+    args = ap.parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        return launch_ranks(args, argv)
+    return run_rank(args)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

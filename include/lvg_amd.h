@@ -332,10 +332,22 @@ int         lvg_last_kernel_time(const lvg_handle *h, double *ms, int *nb_launch
 
 /* Milliseconds of the collision-operator kernel (coll_kernel) that ran ahead of
  * the solve kernel in the last lvg_solve_layers* call, 0 if it did not run
- * (wave kernel, warm chains, LVG_COLL_AHEAD=0 or over the memory budget). The
+ * (the default; wave kernel, warm chains, or the batch over its memory budget). The
  * reference builds these operators inside set_gas_param per layer
  * (coll_rates.cpp:152-174, iteration_lvg.cpp:121-131); no reference counterpart. */
 int         lvg_last_coll_time(const lvg_handle *h, double *ms);
+
+/* Tuning and diagnostics of this handle: "key=value,key=value" (NULL or "" = the
+ * defaults); the environment variable LVG_TUNING supplies the initial value at
+ * lvg_create. No setting changes a result (populations and status stay bit-identical).
+ * Keys: block_kernel (1: the block kernel also for N <= 64), queue_order (0: layer
+ * order instead of longest-expected-first), coll_ahead (1: collision operators of the
+ * batch built ahead by a separate kernel), coll_mem (fraction of free device memory
+ * that batch may take, default 0.5), coll_order (0: that kernel in layer order),
+ * blocks_per_cu (resident block-kernel workgroups per CU, 0 = automatic).
+ * LVG_E_ARG on an unknown key or value (the tuning is then unchanged). No reference
+ * counterpart (the reference has no device). */
+int         lvg_set_tuning(lvg_handle *h, const char *spec);
 
 #ifdef __cplusplus
 }

@@ -65,6 +65,18 @@ struct ModeHost {
 
 }  // namespace
 
+// Tuning and diagnostics (not results: every setting gives bit-identical populations and
+// status). Defaults, then the LVG_TUNING environment variable once at lvg_create, then
+// lvg_set_tuning; the format is "key=value,key=value" with the keys below.
+struct LvgTuning {
+    int block_kernel = 0;      // block_kernel=1: the block kernel also for N <= 64
+    int queue_order = 1;       // queue_order=0: work queue in layer order, not longest-expected-first
+    int coll_ahead = 0;        // coll_ahead=1: coll_kernel builds the batch's collision operators ahead
+    double coll_mem = 0.5;     // coll_mem=f: ... when they fit this fraction of the free device memory
+    int coll_order = 1;        // coll_order=0: coll_kernel in layer order, not temperature order
+    int blocks_per_cu = 0;     // blocks_per_cu=k: resident block-kernel workgroups per CU (0: automatic)
+};
+
 struct lvg_handle {
     int device = 0;
     int N = 0;
@@ -111,6 +123,7 @@ struct lvg_handle {
     LvgDevProblem *d_prob = nullptr;
     LvgLaunch *d_launch = nullptr;
     int n_launch_slots = 0;
+    LvgTuning tune;
     std::string err;
 };
 
@@ -124,6 +137,34 @@ int fail(lvg_handle *h, int code, const char *fmt, ...) {
     va_end(ap);
     if (h) h->err = buf; else g_create_error = buf;
     return code;
+}
+
+// "key=value,key=value" onto t (keys of LvgTuning); LVG_E_ARG on anything else
+int parse_tuning(lvg_handle *h, const char *spec, LvgTuning &t) {
+    if (!spec) return LVG_OK;
+    std::string s(spec);
+    size_t i = 0;
+    while (i < s.size()) {
+        size_t j = s.find(',', i);
+        if (j == std::string::npos) j = s.size();
+        const std::string item = s.substr(i, j - i);
+        i = j + 1;
+        if (item.empty()) continue;
+        const size_t eq = item.find('=');
+        if (eq == std::string::npos) return fail(h, LVG_E_ARG, "tuning item '%s' is not key=value", item.c_str());
+        const std::string k = item.substr(0, eq), v = item.substr(eq + 1);
+        char *end = nullptr;
+        const double x = std::strtod(v.c_str(), &end);
+        if (v.empty() || *end) return fail(h, LVG_E_ARG, "tuning value '%s' is not a number", v.c_str());
+        if (k == "block_kernel") t.block_kernel = x != 0.;
+        else if (k == "queue_order") t.queue_order = x != 0.;
+        else if (k == "coll_ahead") t.coll_ahead = x != 0.;
+        else if (k == "coll_mem" && x >= 0. && x <= 1.) t.coll_mem = x;
+        else if (k == "coll_order") t.coll_order = x != 0.;
+        else if (k == "blocks_per_cu" && x >= 0. && x <= 8.) t.blocks_per_cu = (int)x;
+        else return fail(h, LVG_E_ARG, "unknown tuning key or bad value '%s'", item.c_str());
+    }
+    return LVG_OK;
 }
 
 #define HIPCHECK(h, x)                                                                   \
@@ -647,11 +688,35 @@ int grow(lvg_handle *h, void **p, size_t *cap, size_t bytes) {
     return LVG_OK;
 }
 
+// grow() without an error: false (and the buffer released) if the allocation fails
+bool try_grow(lvg_handle *h, void **p, size_t *cap, size_t bytes) {
+    if (bytes <= *cap) return true;
+    drain(h);
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc(p, bytes) != hipSuccess) {
+        (void)hipGetLastError();     // clear the sticky allocation error
+        *p = nullptr;
+        return false;
+    }
+    *cap = bytes;
+    return true;
+}
+
 }  // namespace
 
 extern "C" {
 
 int lvg_abi_version(void) { return LVG_ABI_VERSION; }
+
+int lvg_set_tuning(lvg_handle *h, const char *spec) {
+    if (!h) return LVG_E_STATE;
+    LvgTuning t;
+    const int rc = parse_tuning(h, spec, t);
+    if (rc == LVG_OK) h->tune = t;
+    return rc;
+}
 
 void lvg_solve_opts_default(lvg_solve_opts *o) {
     if (!o) return;
@@ -705,6 +770,7 @@ int lvg_create(const lvg_problem *prob, int device, lvg_handle **out) {
     lvg_handle *h = new (std::nothrow) lvg_handle();
     if (!h) return fail(nullptr, LVG_E_NOMEM, "out of host memory");
     int rc = validate(h, prob);
+    if (rc == LVG_OK) rc = parse_tuning(h, std::getenv("LVG_TUNING"), h->tune);
     if (rc == LVG_OK) {
         h->device = device;
         hipError_t e = hipSetDevice(device);
@@ -750,6 +816,7 @@ namespace {
 
 // chain_off: host [nb_chain + 1] (warm chains) or NULL (independent layers)
 int check_chains(lvg_handle *h, int nb_lay, int nb_chain, const int *chain_off) {
+    if (nb_lay == 0 && nb_chain == 0) return LVG_OK;     // an empty batch (e.g. a rank with no clouds)
     if (nb_chain < 1 || !chain_off) return fail(h, LVG_E_ARG, "warm chains need nb_chain >= 1 and chain_off");
     if (chain_off[0] != 0 || chain_off[nb_chain] != nb_lay)
         return fail(h, LVG_E_ARG, "chain_off must start at 0 and end at nb_lay");
@@ -776,20 +843,16 @@ int launch_solve(lvg_handle *h, int nb_lay, const double *d_soa, double *d_pops,
     // for warm chains, whose items are long and even: 512 chains of 8 layers take 57.7 ms
     // at one workgroup per CU against 39.8 ms at two.
     if (!chain_off && nq <= 2 * h->cus) per_cu = 1;
-    if (const char *e = std::getenv("LVG_BLOCKS_PER_CU")) {   // tuning/diagnostics only
-        const int v = std::atoi(e);
-        if (v >= 1 && v <= h->blocks_per_cu) per_cu = v;
-    }
-    // kernel choice: one wave per layer for N <= 64 (lvg_wave.h), else one block per layer.
-    // Both give bit-identical results; LVG_BLOCK_KERNEL=1 forces the block kernel.
+    if (h->tune.blocks_per_cu >= 1 && h->tune.blocks_per_cu <= h->blocks_per_cu) per_cu = h->tune.blocks_per_cu;
+    // kernel choice: one wave per layer for N <= 64 (lvg_wave.hip), else one block per layer.
+    // Both give bit-identical results; tuning block_kernel=1 forces the block kernel.
     int wpb = 0, wave_bpc = 0;
     size_t wdyn = 0;
     {
         const LvgModeLines &mh = o->line_overlap ? h->P.overlap : h->P.plain;
         const int grid_dbl = h->P.esc_nd + h->P.esc_ng +
                              (o->line_overlap ? h->P.ov_nd + h->P.ov_ndx + h->P.ov_ngr + h->P.ov_ng : 0);
-        const char *force = std::getenv("LVG_BLOCK_KERNEL");
-        if (!(force && force[0] == '1') && lvg_wave_plan(h->N, 2 * mh.nb_lines, grid_dbl, h->lds_cap, &wpb, &wdyn) &&
+        if (!h->tune.block_kernel && lvg_wave_plan(h->N, 2 * mh.nb_lines, grid_dbl, h->lds_cap, &wpb, &wdyn) &&
             lvg_wave_occupancy(h->N, wpb, wdyn, &wave_bpc) == hipSuccess && wave_bpc >= 1) {
         } else {
             wpb = 0;
@@ -826,7 +889,7 @@ int launch_solve(lvg_handle *h, int nb_lay, const double *d_soa, double *d_pops,
         L.chain_off = h->d_chain;
         L.nb_chain = nb_chain;
         L.order = h->d_chain + nb_chain + 1;
-    } else if (nb_lay > slots && !std::getenv("LVG_INDEX_ORDER")) {
+    } else if (nb_lay > slots && h->tune.queue_order) {
         // longest-expected-first order of the work queue (lvg_sched.hip); results do not
         // depend on it. Scratch: keys, sorted keys (double), indices, order (int).
         size_t tmp = 0;
@@ -839,26 +902,25 @@ int launch_solve(lvg_handle *h, int nb_lay, const double *d_soa, double *d_pops,
         L.order = order;
     }
     // independent layers on the block kernels: collision operators of the whole batch
-    // built ahead by coll_kernel into HBM (K, and B for the boundary-layer start) when
-    // they fit the budget (LVG_COLL_AHEAD=0 disables; LVG_COLL_AHEAD_GB, default 64)
+    // built ahead by coll_kernel into HBM (K, and B for the boundary-layer start) when the
+    // tuning asks for it and they fit coll_mem of the free device memory; if the buffer
+    // cannot be had, every layer builds its own in the solve kernel (same results)
     bool coll_ahead = false;
-    if (!wave && !chain_off) {
-        const char *e = std::getenv("LVG_COLL_AHEAD");
-        const char *g = std::getenv("LVG_COLL_AHEAD_GB");
-        const double cap_gb = g ? std::atof(g) : 64.;
+    if (!wave && !chain_off && h->tune.coll_ahead) {
         const bool need_b = o->init != LVG_INIT_GIVEN;
         const bool b_from_k = h->P.nb_tables == h->P.nb_neutral;   // no electron tables: B = f(K)
         const size_t nn = (size_t)nb_lay * h->N * h->N * sizeof(double);
         const size_t nd = (size_t)nb_lay * h->N * sizeof(double);
         const size_t bytes = nn + (need_b ? (b_from_k ? nd : nn) : 0);
-        if (!(e && e[0] == '0') && (double)bytes <= cap_gb * 1073741824.) {
-            if ((rc = grow(h, &h->d_coll, &h->coll_cap, bytes))) return rc;
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+        if ((double)bytes <= h->tune.coll_mem * (double)(free_b + h->coll_cap) && try_grow(h, &h->d_coll, &h->coll_cap, bytes)) {
             L.kall = static_cast<const double *>(h->d_coll);
             const double *tail = static_cast<const double *>(h->d_coll) + nn / sizeof(double);
             L.ball = (need_b && !b_from_k) ? tail : nullptr;
             L.bdiag = (need_b && b_from_k) ? tail : nullptr;
             coll_ahead = true;
-            if (!std::getenv("LVG_COLL_INDEX_ORDER")) {
+            if (h->tune.coll_order) {
                 // temperature order for coll_kernel (lvg_sched.hip); its own scratch, since
                 // the solve queue's order may live in d_sched
                 size_t tmp = 0;
@@ -873,6 +935,13 @@ int launch_solve(lvg_handle *h, int nb_lay, const double *d_soa, double *d_pops,
                 L.coll_order = ord;
             }
         }
+    }
+    if (!coll_ahead && h->d_coll) {
+        // the batch buffer of an earlier call is not held across calls that do not use it
+        drain(h);
+        (void)hipFree(h->d_coll);
+        h->d_coll = nullptr;
+        h->coll_cap = 0;
     }
     const LvgLaunch *dL = nullptr;
     if ((rc = push_launch(h, L, 0, s, &dL))) return rc;

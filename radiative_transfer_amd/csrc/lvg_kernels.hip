@@ -1,23 +1,28 @@
-// lvg_kernels.hip — MI355X (gfx950) kernels of the LVG level-population solver.
+// lvg_kernels.hip — MI355X (gfx950) block kernels of the LVG level-population solver.
 //
-// One 256-thread workgroup owns one cloud layer at a time and runs the whole
-// reference per-layer pipeline on the device (radiative_transfer.cpp:236-288):
-// layer parameters (iteration_lvg.cpp:59-85), collision operator
-// (coll_rates*.cpp get_rate_*), boundary_layer_populations (iteration_control.cpp:52-91),
-// the iteration_control fixed-point loop with Ng acceleration
-// (iteration_control.h:84-242), and per iteration the rate-matrix assembly,
-// residual and LU solve of calc_new_pop (iteration_lvg.cpp:87-161).
+// One workgroup owns one cloud layer at a time and runs the whole reference per-layer
+// pipeline on the device (radiative_transfer.cpp:236-288): layer parameters
+// (iteration_lvg.cpp:59-85), collision operator (coll_rates*.cpp get_rate_*),
+// boundary_layer_populations (iteration_control.cpp:52-91), the iteration_control
+// fixed-point loop with Ng acceleration (iteration_control.h:84-242), and per iteration
+// the rate-matrix assembly, residual and LU solve of calc_new_pop (iteration_lvg.cpp:87-161).
 //
-// The grid is persistent: blocks pull layers from an atomic work queue, so
-// layers with very different iteration counts balance across CUs, and each
-// block's scratch (collision operator K, working matrix A, Ng history) lives in
-// a per-slot HBM workspace.
+// The grid is persistent: blocks pull layers from an atomic work queue, so layers with
+// very different iteration counts balance across CUs, and each block's scratch
+// (collision operator K, working matrix A, Ng history) lives in a per-slot HBM workspace.
 //
-// fp64 throughout, no MFMA. Bit-exact with the CPU oracle by construction: this
-// file is compiled with -ffp-contract=off, every operation follows the oracle's
-// order, and the only fused multiply-adds are the explicit fma() of the LU,
-// whose per-element update sequence (k ascending) the blocked factorization
-// preserves.
+// fp64 throughout, no MFMA. Bit-exact with the CPU oracle by construction: this file is
+// compiled with -ffp-contract=off, every operation follows the oracle's order, and the
+// only fused multiply-adds are the explicit fma() of the LU, whose per-element update
+// sequence (k ascending) the blocked factorization preserves.
+//
+// Instantiation. The product library compiles this file twice: as is (namespace lvg,
+// 256 threads, N <= 256, 2 workgroups per CU) and through lvg_kernels_big.hip (LVG_BIG:
+// namespace lvg_big, 768 threads, N <= 768 — the reference's CH3OH callers,
+// radiative_transfer.cpp:647, :773 — one workgroup per CU, the whole LDS). The
+// algorithm, the operation order and hence the results are the same; every extern "C"
+// entry of the second copy carries the suffix _big. The wave-per-layer kernel for
+// N <= 64 is lvg_wave.hip.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
@@ -26,123 +31,37 @@
 #include "../../include/lvg_amd.h"
 #include "../../include/lvg_math.h"
 
-// Instantiation. The product library compiles this file twice: as is (namespace lvg,
-// 256 threads, N <= 256, 2 workgroups per CU) and through lvg_kernels_big.hip
-// (LVG_BIG: namespace lvg_big, 768 threads, N <= 768 — the reference's CH3OH
-// callers, radiative_transfer.cpp:647, :773 — one workgroup per CU, the whole LDS).
-// The algorithm, the operation order and hence the results are the same; every
-// extern "C" entry of the second copy carries the suffix _big.
 #ifndef LVG_BIG
 #define LVG_BIG 0
 #endif
 #if LVG_BIG
 #define LVG_NS lvg_big
 #define LVG_SYM(name) name##_big
-#ifndef LVG_BT
-#define LVG_BT 768
-#endif
-#ifndef LVG_NMAX
-#define LVG_NMAX 768
-#endif
-#ifndef LVG_OCC
-#define LVG_OCC 1
-#endif
 #else
 #define LVG_NS lvg
 #define LVG_SYM(name) name
-#ifndef LVG_BT
-#define LVG_BT 256
-#endif
-#ifndef LVG_NMAX
-#define LVG_NMAX 256
-#endif
 #endif
 
 namespace LVG_NS {
 
-// Diagnostic build only (-DLVG_PHASE_TIMERS): per-phase s_memtime cycle sums,
-// thread 0 of every block, flushed to lvg_phase_cycles[]. Never in the product .so.
-#ifdef LVG_PHASE_TIMERS
-enum { PH_SETUP, PH_BOUNDARY, PH_LINES, PH_ASSEMBLE, PH_PANEL, PH_TRSM, PH_GEMM, PH_BACKSUB, PH_CTL,
-       PH_LSETUP, PH_PAIRS, PH_BDIAG, PH_BLOAD, PH_CLK_MEMTIME, PH_CLK_REALTIME, PH_RSV,
-       PH_T_FETCH, PH_T_SOLVE, PH_T_STAGE, PH_P_RED, PH_P_POST, PH_P_WB, PH_N };
-__device__ unsigned long long lvg_phase_cycles[32];
-#define TSTAMP(v) unsigned long long v = __builtin_amdgcn_s_memtime()
-#define RSTAMP(v) unsigned long long v = __builtin_amdgcn_s_memrealtime()
-// sums kept in LDS by thread 0 (no global atomics inside the timed code: queued
-// atomics would hold up the vmcnt waits of later loads), flushed once per block
-__shared__ unsigned long long lvg_ph_lds[32];
-#define RACC(ph, v0) do { if (threadIdx.x == 0) { unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); \
-    lvg_ph_lds[ph] += t_ - (v0); } } while (0)
-#define TACC(ph, v0) do { if (threadIdx.x == 0) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-    lvg_ph_lds[ph] += t_ - (v0); } } while (0)
-#define PH_INIT() do { if (threadIdx.x < 32) lvg_ph_lds[threadIdx.x] = 0; __syncthreads(); } while (0)
-#define PH_FLUSH() do { __syncthreads(); if (threadIdx.x < 32 && lvg_ph_lds[threadIdx.x]) \
-    atomicAdd(&lvg_phase_cycles[threadIdx.x], lvg_ph_lds[threadIdx.x]); } while (0)
-#else
-#define TSTAMP(v) do {} while (0)
-#define TACC(ph, v0) do {} while (0)
-#define RSTAMP(v) do {} while (0)
-#define RACC(ph, v0) do {} while (0)
-#define PH_INIT() do {} while (0)
-#define PH_FLUSH() do {} while (0)
-#endif
+#include "lvg_common.h"
 
-constexpr int BT   = LVG_BT;     // threads per workgroup (one panel row per thread: N <= BT)
+constexpr int BT   = LVG_BIG ? 768 : 256;   // threads per workgroup (one panel row per thread: N <= BT)
+constexpr int NMAX = BT;                    // max levels of this kernel
+constexpr int OCC  = LVG_BIG ? 1 : 2;       // resident workgroups per CU the kernel is built for
 constexpr int NW   = BT / 64;
-constexpr int NB   = 16;         // LU panel width
-constexpr int NMAX = LVG_NMAX;   // max levels of this kernel
+constexpr int NB   = 16;                    // LU panel width (chunk)
 static_assert(NMAX <= BT && BT % 64 == 0 && NMAX % 32 == 0, "one row per thread, whole waves");
-constexpr int NHIST = LVG_HIST_SLOTS;
-
-constexpr double BOLTZMANN_CONSTANT    = 1.380649e-16;
-constexpr double CM_INVERSE_TO_KELVINS = 1.438776877;
-constexpr double EIGHT_PI              = 25.132741228718345;
-constexpr double SPEED_OF_LIGHT        = 2.99792458e+10;
-constexpr double MIN_COLLISION_RATE    = 1.e-99;
-constexpr double INV_TRANS_FACTOR      = -0.1;
-constexpr double MIN_LINE_OPACITY      = 1.e-99;
-
-#ifndef LVG_PREFETCH_L
-#define LVG_PREFETCH_L 0
-#endif
-#ifndef LVG_GEMM_PIPE
-#define LVG_GEMM_PIPE 0
-#endif
-#ifndef LVG_PANEL_W1
-#define LVG_PANEL_W1 0
-#endif
-#ifndef LVG_PANEL_PRIO
-#define LVG_PANEL_PRIO 0
-#endif
-#ifndef LVG_UB2
-#define LVG_UB2 1                     // Ub double-buffered by chunk parity: 2 barriers per earlier-chunk step, not 3
-#endif
-#ifndef LVG_L11_ROWS
-#define LVG_L11_ROWS 0
-#endif
-#ifndef LVG_LA_TILE
-#define LVG_LA_TILE 1
-#endif
-#ifndef LVG_PANEL_ONEWAVE
-#define LVG_PANEL_ONEWAVE 2
-#endif
-#ifndef LVG_OCC
-#define LVG_OCC 2                     // resident workgroups per CU solve_kernel is built for
-#endif
-constexpr int YCAP = (LVG_OCC >= 3 || LVG_BIG) ? 1 : 2048;   // line terms kept in LDS when 2*nb_lines <= YCAP
-#ifndef LVG_TC
-#define LVG_TC 4
-#endif
-constexpr int TC = LVG_TC;            // columns per thread in the LU register tile (TR rows x TC); 4 or 2
-static_assert(TC == 4 || TC == 2, "register tile width");
-constexpr int TR = NMAX * 8 / BT;     // tile rows per thread: the BT/8 row groups cover NMAX
+constexpr int YCAP = LVG_BIG ? 1 : 2048;    // line terms kept in LDS when 2*nb_lines <= YCAP
+constexpr int TC = 4;                       // columns per thread in the LU register tile (TR rows x TC)
+constexpr int TR = NMAX * 8 / BT;           // tile rows per thread: the BT/8 row groups cover NMAX
 static_assert(TR * (BT / 8) >= NMAX && TR % 2 == 0, "the register tiles cover every row");
-constexpr int WB = 8 * TC;            // LU block-column width
+constexpr int WB = 8 * TC;                  // LU block-column width
+constexpr int COLL_PU = 4;                  // 16x16 pair tiles per batch of the in-kernel collision build
 
 struct Smem {
     double pold[NMAX], bvec[NMAX];
-#if LVG_OCC >= 3 || LVG_BIG
+#if LVG_BIG
     union { double pnew[NMAX]; double blog[NMAX]; };   // pnew only ever copies blog
 #else
     double pnew[NMAX], blog[NMAX];
@@ -180,81 +99,6 @@ struct Smem {
     int    layer, pidx;
 };
 
-// ------------------------------------------------------------------------------
-// small helpers
-// ------------------------------------------------------------------------------
-// L2 prefetch: an ordinary dword load whose value is kept alive by an empty asm
-// use; the compiler tracks it like any load (vmcnt), so no VGPR is reused early.
-#ifndef LVG_GEMM_B128
-#define LVG_GEMM_B128 1
-#endif
-#ifndef LVG_PANEL_BALLOT
-#define LVG_PANEL_BALLOT 1
-#endif
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
-    return v;
-}
-
-// ---- DPP wave reductions (gfx9 row_shr / row_bcast sequence; the result lands in
-//      lane 63 and is broadcast with readlane). old == src makes lanes without a
-//      DPP source keep their own value, the identity of max/min.
-template <int CTRL, int ROW, int BANK>
-__device__ __forceinline__ double dpp_d(double x) {
-    int lo = __double2loint(x), hi = __double2hiint(x);
-    lo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROW, BANK, false);
-    hi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROW, BANK, false);
-    return __hiloint2double(hi, lo);
-}
-template <int CTRL, int ROW, int BANK>
-__device__ __forceinline__ int dpp_i(int x) {
-    return __builtin_amdgcn_update_dpp(x, x, CTRL, ROW, BANK, false);
-}
-template <int CTRL, int ROW, int BANK>
-__device__ __forceinline__ unsigned dpp_u0(unsigned x) {   // out-of-row lanes read 0 (bound_ctrl)
-    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROW, BANK, true);
-}
-// wave-wide unsigned max; each step folds into one v_max_u32_dpp
-__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
-    v = max(v, dpp_u0<0x111, 0xf, 0xf>(v));   // row_shr:1
-    v = max(v, dpp_u0<0x112, 0xf, 0xf>(v));   // row_shr:2
-    v = max(v, dpp_u0<0x113, 0xf, 0xf>(v));   // row_shr:3
-    v = max(v, dpp_u0<0x114, 0xf, 0xe>(v));   // row_shr:4
-    v = max(v, dpp_u0<0x118, 0xf, 0xc>(v));   // row_shr:8
-    v = max(v, dpp_u0<0x142, 0xa, 0xf>(v));   // row_bcast:15
-    v = max(v, dpp_u0<0x143, 0xc, 0xf>(v));   // row_bcast:31
-    return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
-}
-
-__device__ __forceinline__ double wave_max_dpp(double v) {
-    v = fmax(v, dpp_d<0x111, 0xf, 0xf>(v));   // row_shr:1
-    v = fmax(v, dpp_d<0x112, 0xf, 0xf>(v));   // row_shr:2
-    v = fmax(v, dpp_d<0x113, 0xf, 0xf>(v));   // row_shr:3
-    v = fmax(v, dpp_d<0x114, 0xf, 0xe>(v));   // row_shr:4
-    v = fmax(v, dpp_d<0x118, 0xf, 0xc>(v));   // row_shr:8
-    v = fmax(v, dpp_d<0x142, 0xa, 0xf>(v));   // row_bcast:15
-    v = fmax(v, dpp_d<0x143, 0xc, 0xf>(v));   // row_bcast:31
-    int lo = __builtin_amdgcn_readlane(__double2loint(v), 63);
-    int hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
-    return __hiloint2double(hi, lo);
-}
-__device__ __forceinline__ int wave_min_dpp(int v) {
-    v = min(v, dpp_i<0x111, 0xf, 0xf>(v));
-    v = min(v, dpp_i<0x112, 0xf, 0xf>(v));
-    v = min(v, dpp_i<0x113, 0xf, 0xf>(v));
-    v = min(v, dpp_i<0x114, 0xf, 0xe>(v));
-    v = min(v, dpp_i<0x118, 0xf, 0xc>(v));
-    v = min(v, dpp_i<0x142, 0xa, 0xf>(v));
-    v = min(v, dpp_i<0x143, 0xc, 0xf>(v));
-    return __builtin_amdgcn_readlane(v, 63);
-}
-__device__ __forceinline__ double readlane_d(double x, int lane) {
-    int lo = __builtin_amdgcn_readlane(__double2loint(x), lane);
-    int hi = __builtin_amdgcn_readlane(__double2hiint(x), lane);
-    return __hiloint2double(hi, lo);
-}
-
 __device__ __forceinline__ double block_max(double v, Smem &sm) {
     const int t = threadIdx.x, w = t >> 6;
     v = wave_max(v);
@@ -267,415 +111,18 @@ __device__ __forceinline__ double block_max(double v, Smem &sm) {
     return r;
 }
 
-// argmax with ties to the smallest index (the oracle's first-maximum rule)
-__device__ __forceinline__ int block_argmax(double v, int idx, Smem &sm) {
-    const int t = threadIdx.x, w = t >> 6;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        double ov = __shfl_xor(v, o);
-        int oi = __shfl_xor(idx, o);
-        if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
-    }
-    if ((t & 63) == 0) { sm.red[w] = v; sm.ired[w] = idx; }
-    __syncthreads();
-    double bv = sm.red[0];
-    int bi = sm.ired[0];
-#pragma unroll
-    for (int i = 1; i < NW; i++) {
-        double ov = sm.red[i];
-        int oi = sm.ired[i];
-        if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-    }
-    return bi;
-}
-
-// locate_index restatement: -1 below, n-1 above, else a[j] <= x < a[j+1]
-__device__ __forceinline__ int locate_index(const double *a, int n, double x) {
-    if (x < a[0]) return -1;
-    if (x > a[n - 1]) return n - 1;
-    int l = 0, r = n - 1;
-    while (r - l > 1) {
-        int m = l + ((r - l) >> 1);
-        if (a[m] <= x) l = m; else r = m;
-    }
-    return l;
-}
-
-// lvg_method_data::get_esc_func (lvg_method_functions.cpp:74-110)
-// Grids the escape-probability lookups bisect: the problem's global copies (block
-// kernel) or LDS copies (wave kernel, lvg_wave.h); the tables stay in HBM/L2.
-struct EscGrids {
-    const double *ed, *eg;                 // esc_delta, esc_gamma
-    const double *old, *odx, *ogr, *og;    // ov_ld, ov_dx, ov_gr, ov_g
-};
-__device__ __forceinline__ EscGrids global_grids(const LvgDevProblem &P) {
-    return EscGrids{P.esc_delta, P.esc_gamma, P.ov_ld, P.ov_dx, P.ov_gr, P.ov_g};
-}
-
-__device__ __forceinline__ double esc_func(const LvgDevProblem &P, const EscGrids &G, double gamma, double delta) {
-    const int nd = P.esc_nd, ng = P.esc_ng;
-    int k = locate_index(G.ed, nd, delta);
-    int l = locate_index(G.eg, ng, gamma);
-    double t, u;
-    if (k < 0) { t = 0.; k = 0; }
-    else if (k > nd - 2) { t = 1.; k = nd - 2; }
-    else t = (delta - G.ed[k]) / (G.ed[k + 1] - G.ed[k]);
-    if (l < 0) { l = 0; u = 0.; }
-    else if (l > ng - 2) { l = ng - 2; u = 1.; }
-    else u = (gamma - G.eg[l]) / (G.eg[l + 1] - G.eg[l]);
-    const double *p = P.esc_p;
-    double e = p[k * ng + l] * (1. - t) * (1. - u) + p[(k + 1) * ng + l] * t * (1. - u)
-             + p[k * ng + l + 1] * (1. - t) * u + p[(k + 1) * ng + l + 1] * u * t;
-    return e > 1. ? 1. : (e < 0. ? 0. : e);
-}
-
-// lvg_line_overlap_data::get_esc_func (lvg_method_functions.cpp:324-392); the
-// 16 terms in the reference's order, each weighted (u, t, p, y) left to right
-__device__ __forceinline__ double overlap_esc_func(const LvgDevProblem &P, const EscGrids &G, const double *tab,
-                                                   double gamma, double delta, double gratio, double dxv) {
-    delta = lvg_log10(delta);
-    int m = locate_index(G.old, P.ov_nd, delta);
-    int l = locate_index(G.og, P.ov_ng, gamma);
-    int k = locate_index(G.ogr, P.ov_ngr, gratio);
-    int n = locate_index(G.odx, P.ov_ndx, dxv);
-    double y = 0., u = 0., t = 0., p = 0.;
-    if (m < 0) m = 0;
-    else if (m > P.ov_nd - 2) { m = P.ov_nd - 2; y = 1.; }
-    else y = (delta - G.old[m]) / (G.old[m + 1] - G.old[m]);
-    if (n < 0) n = 0;
-    else if (n > P.ov_ndx - 2) { p = 1.; n = P.ov_ndx - 2; }
-    else p = (dxv - G.odx[n]) / (G.odx[n + 1] - G.odx[n]);
-    if (l < 0) l = 0;
-    else if (l > P.ov_ng - 2) { l = P.ov_ng - 2; u = 1.; }
-    else u = (gamma - G.og[l]) / (G.og[l + 1] - G.og[l]);
-    if (k < 0) k = 0;
-    else if (k > P.ov_ngr - 2) { t = 1.; k = P.ov_ngr - 2; }
-    else t = (gratio - G.ogr[k]) / (G.ogr[k + 1] - G.ogr[k]);
-    const int W = P.ov_ngr * P.ov_ng, ndx = P.ov_ndx, ng = P.ov_ng;
-    double e = 0.;
-#pragma unroll
-    for (int dm = 0; dm < 2; dm++)
-#pragma unroll
-        for (int dn = 0; dn < 2; dn++)
-#pragma unroll
-            for (int dk = 0; dk < 2; dk++)
-#pragma unroll
-                for (int dl = 0; dl < 2; dl++)
-                    e += tab[(int64_t)((m + dm) * ndx + n + dn) * W + (k + dk) * ng + l + dl]
-                         * (dl ? u : 1. - u) * (dk ? t : 1. - t) * (dn ? p : 1. - p) * (dm ? y : 1. - y);
-    return e > 1. ? 1. : (e < 0. ? 0. : e);
-}
-
-// ------------------------------------------------------------------------------
-// layer setup: iteration_scheme_lvg::set_parameters / set_gas_param
-// ------------------------------------------------------------------------------
-// the layer's scalars into sm (one thread; SM: Smem or the wave kernel's WaveLayer)
-template <class SM>
-__device__ __forceinline__ void layer_scalars(const LvgDevProblem &P, const LvgLaunch &Lc, int l, SM &sm) {
-    {
-        const int64_t ld = Lc.soa_ld;
-        const double *s = Lc.soa + Lc.lay_offset + l;
-        double T = s[0 * ld], Te = s[1 * ld];
-        double ne = s[2 * ld], nh = s[3 * ld], nph2 = s[4 * ld], noh2 = s[5 * ld], nhe = s[6 * ld];
-        double vt = s[8 * ld];
-        sm.T = T; sm.Te = Te;
-        sm.nmol = s[7 * ld];
-        sm.ne = ne;
-        sm.vgrad = s[9 * ld];
-        sm.vw = sqrt(2. * BOLTZMANN_CONSTANT * T / P.mass + vt * vt);   // iteration_lvg.cpp:65
-        for (int c = 0; c < P.nb_comp; c++) sm.dust[c] = s[(10 + c) * ld];
-        const double n5[5] = {nhe, nph2, noh2, nh, ne};
-        for (int k = 0; k < P.terms.nb_combos; k++) {
-            double a = 0.;
-            bool first = true;
-            for (int q = 0; q < 5; q++) {
-                double w = P.terms.combo_w[k][q];
-                if (w == 0.) continue;
-                double term = (w == 1.) ? n5[q] : w * n5[q];
-                a = first ? term : a + term;
-                first = false;
-            }
-            sm.cc[k] = a;
-        }
-        for (int tb = 0; tb < P.nb_tables; tb++) {
-            const double *tg = P.tab_tgrid + P.tab_tg_off[tb];
-            int jm = P.tab_jmax[tb];
-            double temp = (tb < P.nb_neutral) ? T : Te;
-            int lo = 0, hi = jm - 1;                  // collision_data::locate, strict '<'
-            while (hi - lo > 1) {
-                int j = lo + ((hi - lo) >> 1);
-                if (tg[j] < temp) lo = j; else hi = j;
-            }
-            sm.lo[tb] = lo;
-            double tmax = tg[jm - 1];
-            sm.teff[tb] = temp < tmax ? temp : tmax;
-            const int64_t imax = (int64_t)P.tab_nb_lev[tb] * (P.tab_nb_lev[tb] - 1) / 2;
-            sm.timax[tb] = imax;
-            sm.tcol[tb] = P.tab_coeff + P.tab_c_off[tb] + (int64_t)lo * imax;
-            sm.tder[tb] = P.tab_deriv + P.tab_c_off[tb] + (int64_t)lo * imax;
-            sm.tdt[tb] = tg[lo + 1] - tg[lo];
-            sm.tx[tb] = sm.teff[tb] - tg[lo];
-        }
-    }
-}
-
 __device__ __forceinline__ void layer_setup(const LvgDevProblem &P, const LvgLaunch &Lc, int l, Smem &sm) {
     if (threadIdx.x == 0) layer_scalars(P, Lc, l, sm);
     __syncthreads();
 }
 
-// the compiled molecule rule, copied to LDS once per launch
-template <class SM>
-__device__ __forceinline__ void load_rule_table(const LvgDevProblem &P, SM &sm) {
-    for (int e = threadIdx.x; e < LVG_MAX_CLASSES * LVG_MAX_TERMS; e += BT) {
-        (&sm.ttab[0][0])[e] = (&P.terms.table[0][0])[e];
-        (&sm.tcombo[0][0])[e] = (&P.terms.combo[0][0])[e];
-    }
-    for (int e = threadIdx.x; e < LVG_MAX_CLASSES; e += BT) {
-        sm.tet[e] = P.terms.etable[e];
-        sm.tgrp[e] = P.terms.group[e];
-    }
-    __syncthreads();
-}
-
-// Collision operator K (neutral + electron rates; iteration_lvg.cpp:121-131) and
-// the boundary-layer matrix B (neutrals + A/2; iteration_control.cpp:69-85),
-// row-major M[final][initial]. K keeps off-diagonals only (its diagonal is
-// rebuilt every iteration in the reference's order); B gets its diagonal as the
-// ascending column sum, row 0 <- 1. Level pairs (f > s) are walked in 16x16 tiles
-// of the lower triangle, one pair per thread: table reads and the K[f][s] writes
-// are 128-byte row segments, every lane is busy.
-#ifndef LVG_CLS_LDS
-#define LVG_CLS_LDS 1                 // pair classes staged in LDS for the collision build
-#endif
-#ifndef LVG_U_DEFER
-#define LVG_U_DEFER 0                 // 1: LU U stores issued behind the next step's loads (121 VGPRs spill: slower)
-#endif
-#ifndef LVG_COLL_DEFER
-#define LVG_COLL_DEFER 1              // collision build: a batch's stores issued behind the next batch's loads
-#endif
-#ifndef LVG_COLL_PU
-#define LVG_COLL_PU 4                 // 16x16 pair tiles per batch of the collision build
-#endif
-template <class SM, int PU = LVG_COLL_PU>
-__device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P, SM &sm, double *K, double *B,
-                                                          bool electrons = true) {
-    const int N = P.N, t = threadIdx.x;
-    const double T = sm.T, Te = sm.Te;
-    const int nt = (N + 15) >> 4, ntiles = nt * (nt + 1) / 2;
-    const int fl = (t >> 4) & 15, sl = t & 15;
-    TSTAMP(tq0);
-    // the pair classes (one byte per level pair) staged in the LU's panel buffer, which is
-    // free between factorizations, when they fit: one wide coalesced copy instead of a
-    // dependent global load in front of every batch's coefficient loads
-    const int M = N * (N - 1) / 2;
-    const bool cls_lds = LVG_CLS_LDS && M <= (int)sizeof(sm.pu);
-    uint8_t *clsl = reinterpret_cast<uint8_t *>(&sm.pu);
-    if (cls_lds) {
-        const int n16 = M >> 4;
-        const uint4 *src4 = reinterpret_cast<const uint4 *>(P.pair_class);
-        for (int e = t; e < n16; e += BT) reinterpret_cast<uint4 *>(clsl)[e] = src4[e];
-        for (int e = (n16 << 4) + t; e < M; e += BT) clsl[e] = P.pair_class[e];
-        __syncthreads();
-    }
-    // batches of PU tiles: indices and classes, then every coefficient load, then
-    // the arithmetic and the stores (loads never wait behind stores that might alias)
-    constexpr int TG = BT / 256;                     // TG groups of 256 threads, PU tiles each
-    const int tg = t >> 8;
-    // the K/B stores of a batch are issued behind the next batch's loads: vmcnt counts
-    // loads and stores in order, so a load issued after a store waits for it
-    double wk0[PU], wk1[PU], wb0[PU], wb1[PU];
-    int wf[PU], ws[PU];
-#pragma unroll
-    for (int u = 0; u < PU; u++) wf[u] = -1;
-    auto flush = [&]() {
-#pragma unroll
-        for (int u = 0; u < PU; u++) {
-            if (wf[u] >= 0) {
-                const int f = wf[u], s2 = ws[u];
-                K[s2 * N + f] = wk0[u];
-                K[f * N + s2] = wk1[u];
-                if (B) {
-                    B[s2 * N + f] = wb0[u];
-                    B[f * N + s2] = wb1[u];
-                }
-            }
-        }
-    };
-    for (int q0 = 0; q0 < ntiles; q0 += PU * TG) {
-        int pc[PU], fc[PU], sc[PU], cls[PU];
-#pragma unroll
-        for (int u = 0; u < PU; u++) {
-            // tile q = (F, S), S <= F, in row order of the lower triangle of tiles
-            const int q = q0 + tg * PU + u;
-            int F = (int)((sqrt(8. * q + 1.) - 1.) * 0.5);
-            while (F * (F + 1) / 2 > q) F--;
-            while ((F + 1) * (F + 2) / 2 <= q) F++;
-            const int S = q - F * (F + 1) / 2;
-            fc[u] = 16 * F + fl; sc[u] = 16 * S + sl;
-            pc[u] = (q < ntiles && fc[u] < N && sc[u] < fc[u]) ? fc[u] * (fc[u] - 1) / 2 + sc[u] : -1;
-        }
-#pragma unroll
-        for (int u = 0; u < PU; u++) cls[u] = pc[u] < 0 ? 0 : cls_lds ? clsl[pc[u]] : P.pair_class[pc[u]];
-        // level data of the batch, loaded before any store of it
-        double ef[PU], es[PU], gf[PU], gs[PU], af[PU];
-#pragma unroll
-        for (int u = 0; u < PU; u++) {
-            const bool ok = pc[u] >= 0;
-            const int f = ok ? fc[u] : 1, s = ok ? sc[u] : 0;
-            ef[u] = P.energy[f]; es[u] = P.energy[s];
-            gf[u] = P.g[f]; gs[u] = P.g[s];
-            af[u] = B ? P.einst[f * N + s] : 0.;
-        }
-        double c0[PU][LVG_MAX_TERMS + 1], c1[PU][LVG_MAX_TERMS + 1];
-#pragma unroll
-        for (int u = 0; u < PU; u++) {
-            bool alive = pc[u] >= 0;
-#pragma unroll
-            for (int k = 0; k <= LVG_MAX_TERMS; k++) {
-                const int tb = (k < LVG_MAX_TERMS) ? sm.ttab[cls[u]][k] : sm.tet[cls[u]];
-                if (k < LVG_MAX_TERMS) alive = alive && tb >= 0;
-                const bool ld = (k < LVG_MAX_TERMS) ? alive : (pc[u] >= 0 && tb >= 0);
-                c0[u][k] = 0.; c1[u][k] = 0.;
-                if (ld) {
-                    c0[u][k] = sm.tcol[tb][pc[u]];
-                    c1[u][k] = sm.tder[tb][pc[u]];          // slope (calc_coeff_deriv)
-                }
-            }
-        }
-        if (LVG_COLL_DEFER) flush();            // the previous batch's stores, behind this batch's loads
-#pragma unroll
-        for (int u = 0; u < PU; u++) {
-            wf[u] = -1;
-            if (pc[u] < 0) continue;
-            const int cl = cls[u], f = fc[u], s = sc[u];
-            const int grp = sm.tgrp[cl];
-            double dn = 0., gsum = 0.;
-            int ng = 0;
-#pragma unroll
-            for (int k = 0; k < LVG_MAX_TERMS; k++) {
-                const int tb = sm.ttab[cl][k];
-                if (tb < 0) break;
-                const double r = (c0[u][k] + c1[u][k] * sm.tx[tb]) * sm.cc[sm.tcombo[cl][k]];   // get_rate
-                if (k < grp) dn = (k == 0) ? r : dn + r;
-                else { gsum = (ng == 0) ? r : gsum + r; ng++; }
-            }
-            if (ng) dn = dn + gsum;
-            const double de = es[u] - ef[u];
-            double un = 0.;
-            if (dn > MIN_COLLISION_RATE) un = dn * lvg_exp(de * CM_INVERSE_TO_KELVINS / T) * gf[u] / gs[u];
-            else dn = 0.;
-            double dE = 0., uE = 0.;
-            const int et = sm.tet[cl];
-            if (et >= 0 && electrons) {
-                dE = (c0[u][LVG_MAX_TERMS] + c1[u][LVG_MAX_TERMS] * sm.tx[et]) * sm.ne;
-                if (dE > MIN_COLLISION_RATE) uE = dE * lvg_exp(de * CM_INVERSE_TO_KELVINS / Te) * gf[u] / gs[u];
-                else dE = 0.;
-            }
-            wk0[u] = dn + dE;
-            wk1[u] = un + uE;
-            wb0[u] = 0.5 * af[u] + dn;
-            wb1[u] = un;
-            wf[u] = f;
-            ws[u] = s;
-        }
-        if (!LVG_COLL_DEFER) flush();
-    }
-    if (LVG_COLL_DEFER) flush();
-    __syncthreads();
-    TACC(PH_PAIRS, tq0);
-    TSTAMP(tq1);
-    if (B) {
-        for (int d = t; d < N; d += BT) {
-            double a = 0.;
-            for (int r0 = 0; r0 < N; r0 += 32) {
-                double bv[32];
-#pragma unroll
-                for (int u = 0; u < 32; u++) bv[u] = (r0 + u < N) ? B[(r0 + u) * N + d] : 0.;
-#pragma unroll
-                for (int u = 0; u < 32; u++) {
-                    const int r = r0 + u;
-                    if (r < N && r != d) a = a - bv[u];
-                }
-            }
-            B[d * N + d] = a;
-        }
-        __syncthreads();
-        for (int j = t; j < N; j += BT) B[j] = 1.;   // row 0 <- 1 (iteration_control.cpp:82-84)
-        __syncthreads();
-    }
-    TACC(PH_BDIAG, tq1);
-}
-
-// ------------------------------------------------------------------------------
-// radiative terms: intensity_calc (iteration_lvg.cpp:163-185, :428-501)
-// ------------------------------------------------------------------------------
-template <class SM>
-__device__ __forceinline__ double dust_opacity(const LvgDevProblem &P, const LvgModeLines &M, const SM &sm, int n) {
-    double a = 0.;
-    for (int c = 0; c < P.nb_comp; c++) a += M.line_sigma[(int64_t)c * M.nb_lines + n] * sm.dust[c];
-    return a;
-}
-
-template <class SM>
-__device__ __forceinline__ double intensity_single(const LvgDevProblem &P, const EscGrids &G, const LvgModeLines &M,
-                                                   const SM &sm, int n, const double *pop) {
-    const int u = M.line_u[n], l = M.line_l[n];
-    const double energy = M.line_e[n];
-    const double c = sm.nmol / (EIGHT_PI * sm.vw * energy * energy * energy);
-    const double emiss = c * M.line_aul[n] * pop[u];
-    double opac = c * M.line_alu[n] * pop[l] - emiss + MIN_LINE_OPACITY;
-    if (opac < 0.) opac *= INV_TRANS_FACTOR;
-    const double dop = dust_opacity(P, M, sm, n);
-    const double gamma = fabs(sm.vgrad) / (sm.vw * opac);
-    const double delta = fabs(sm.vgrad) / (sm.vw * dop);
-    return emiss / opac * esc_func(P, G, gamma, delta);
-}
-
-template <class SM>
-__device__ __forceinline__ void intensity_pair(const LvgDevProblem &P, const EscGrids &G, const LvgModeLines &M,
-                                               const SM &sm, int n1, int n2, const double *pop, double &i1, double &i2) {
-    const double max_dx = 4.;
-    const int u1 = M.line_u[n1], l1 = M.line_l[n1], u2 = M.line_u[n2], l2 = M.line_l[n2];
-    const double energy = M.line_e[n1];
-    double c = sm.nmol / (EIGHT_PI * sm.vw * energy * energy * energy);
-    const double em1 = c * M.line_aul[n1] * pop[u1];
-    double op1 = c * (M.line_alu[n1] * pop[l1] - M.line_aul[n1] * pop[u1]) + MIN_LINE_OPACITY;
-    const double em2 = c * M.line_aul[n2] * pop[u2];
-    double op2 = c * (M.line_alu[n2] * pop[l2] - M.line_aul[n2] * pop[u2]) + MIN_LINE_OPACITY;
-    if (op1 < 0.) op1 *= INV_TRANS_FACTOR;
-    if (op2 < 0.) op2 *= INV_TRANS_FACTOR;
-    const double g1 = fabs(sm.vgrad) / (sm.vw * op1), g2 = fabs(sm.vgrad) / (sm.vw * op2);
-    const double delta = fabs(sm.vgrad) / (sm.vw * dust_opacity(P, M, sm, n1));
-    double dx = (P.energy[u1] - P.energy[l1] - P.energy[u2] + P.energy[l2]) * SPEED_OF_LIGHT / (energy * sm.vw);
-    if (sm.vgrad < 0.) dx *= -1.;
-    double ep1 = 0., ep2 = 0., ep01 = 0., ep02 = 0.;
-    if (fabs(dx) < max_dx) {
-        ep1 = overlap_esc_func(P, G, P.ov_p1, g1, delta, g2 / g1, dx);
-        ep2 = overlap_esc_func(P, G, P.ov_p1, g2, delta, g1 / g2, -dx);
-    }
-    if (fabs(dx) > max_dx - 0.5) {
-        ep01 = esc_func(P, G, g1, delta);
-        ep02 = esc_func(P, G, g2, delta);
-    }
-    if (fabs(dx) > max_dx) { ep1 = ep01; ep2 = ep02; }
-    else if (fabs(dx) > max_dx - 0.5) {
-        c = 2. * (max_dx - fabs(dx));
-        ep1 = ep01 * (1. - c) + ep1 * c;
-        ep2 = ep02 * (1. - c) + ep2 * c;
-    }
-    i1 = em1 / op1 * ep1;
-    i2 = em2 / op2 * ep2;
-    if (fabs(dx) < max_dx) {
-        ep1 = overlap_esc_func(P, G, P.ov_p2, g1, delta, g2 / g1, dx);
-        ep2 = overlap_esc_func(P, G, P.ov_p2, g2, delta, g1 / g2, -dx);
-        if (fabs(dx) > max_dx - 0.5) {
-            c = 2. * (max_dx - fabs(dx));
-            ep1 *= c; ep2 *= c;
-        }
-        i1 += em2 / op2 * ep1;
-        i2 += em1 / op1 * ep2;
-    }
+// the layer's collision operator K (and the boundary matrix B) in the slot, pair classes
+// staged in the panel buffer, which is free between factorizations, when they fit
+__device__ __forceinline__ void layer_collisions(const LvgDevProblem &P, Smem &sm, double *K, double *B,
+                                                 bool electrons = true) {
+    const int M = P.N * (P.N - 1) / 2;
+    uint8_t *cls = M <= (int)sizeof(sm.pu) ? reinterpret_cast<uint8_t *>(&sm.pu) : nullptr;
+    build_collision_operators<BT, COLL_PU>(P, sm, K, B, cls, electrons);
 }
 
 // y[2n] = A_ul(1+I), y[2n+1] = A_lu*I for every line of the scheme
@@ -757,11 +204,12 @@ struct LuSrc {
 // column and overwritten in place by the factors (L below the pivots, U in the
 // pivot rows), never row-swapped: pivoting is virtual (perm/pos in LDS).
 // Block columns of WB = 32 columns live in registers, an 8x4 fp64 tile per thread
-// (tile rows 8*rg.., cols 4*cg..; tile row r = physical row perm[r] at the block load). For each 16-wide chunk kk to the left (earlier block
-// columns, then the block's own chunks once factored): the chunk's pivot rows are
-// solved against L11 (TRSM -> U rows, stored to A), then every row below is updated
-// with the chunk's L (staged transposed in LDS) and those U rows. Chunks are
-// factored by all four waves, one row per thread in registers (see below).
+// (tile rows 8*rg.., cols 4*cg..; tile row r = physical row perm[r] at the block load).
+// For each 16-wide chunk kk to the left (earlier block columns, then the block's own
+// chunks once factored): the chunk's pivot rows are solved against L11 (TRSM -> U rows,
+// stored to A), then every row below is updated with the chunk's L (staged transposed
+// in LDS) and those U rows. Chunks are factored by all four waves, one row per thread
+// in registers, or by one wave when every active row lies in one or two waves' tile rows.
 //
 // Every element receives fma(-l_ik, u_kj, a_ij) for k ascending and the pivots are
 // chosen from identical values, so the result equals the unblocked, physically
@@ -774,7 +222,6 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
     // right-hand side b[p] in a register; the pivot candidate of each wave publishes
     // its row and its b through LDS.
     const int t = threadIdx.x, w = t >> 6;
-    if (LVG_PANEL_PRIO) __builtin_amdgcn_s_setprio(2);
     double rw[NB];
     const bool valid = t < N;
     const int p = valid ? t : 0;
@@ -788,21 +235,15 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
     for (int c = 0; c < NB; c++) {
         if (c < nb) {
             const int buf = c & 1;
-            // argmax |v| (ties: smallest logical position) as three u32 max reductions:
-            // |v| >= 0 orders like its bit pattern; active rows carry the top bit
-            const double av = fabs(rw[c]);
-            const unsigned long long bits = (act && av == av) ? (unsigned long long)__double_as_longlong(av) : 0ull;
-            // oracle_lu_solve seeds amax with |a_kk| and replaces it on a strict '>': a NaN
-            // below never wins, a NaN on the diagonal (logical position c) always does
-            const bool dnan = act && lp == c && av != av;
-            const unsigned hi = dnan ? 0xffffffffu : act ? ((unsigned)(bits >> 32) | 0x80000000u) : 0u;
-            const unsigned lo = dnan ? 0xffffffffu : (unsigned)bits;
+            // argmax |v| (ties: smallest logical position) as u32 max reductions
+            unsigned hi, lo;
+            pivot_key(rw[c], act, lp == c, hi, lo);
             TSTAMP(tpr);
             const unsigned H = wave_max_u32(hi);
             unsigned Lw;
             int wmin;
-            const unsigned long long tie = LVG_PANEL_BALLOT ? __ballot(hi == H) : 0ull;
-            if (LVG_PANEL_BALLOT && __popcll(tie) == 1) {
+            const unsigned long long tie = __ballot(hi == H);
+            if (__popcll(tie) == 1) {
                 // one lane holds the wave's maximum upper word: it is the candidate
                 const int ln = __ffsll((long long)tie) - 1;
                 Lw = (unsigned)__builtin_amdgcn_readlane((int)lo, ln);
@@ -825,7 +266,7 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
             __syncthreads();                       // one barrier per column
             TACC(PH_P_RED, tpr);
             TSTAMP(tpp);
-            // the four candidates at once, winner picked without branches
+            // the candidates at once, winner picked without branches
             unsigned long long ok[NW];
             int oi[NW];
 #pragma unroll
@@ -867,12 +308,13 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
     __syncthreads();
     if (part) {
         // rows of this chunk and below: factors back to A (physical row p)
-#pragma unroll
-        for (int j = 0; j < NB; j++) if (j < nb && !((N & 1) == 0 && nb == NB)) A[(int64_t)p * N + kk + j] = rw[j];
         if ((N & 1) == 0 && nb == NB) {
             double2 *d2 = reinterpret_cast<double2 *>(A + (int64_t)p * N + kk);
 #pragma unroll
             for (int j = 0; j < NB / 2; j++) d2[j] = make_double2(rw[2 * j], rw[2 * j + 1]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < NB; j++) if (j < nb) A[(int64_t)p * N + kk + j] = rw[j];
         }
         sm.perm[kk + lp] = p;
         sm.pos[p] = kk + lp;
@@ -880,27 +322,22 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
 #pragma unroll
         for (int j = 0; j < NB; j++) sm.pu.P[p][j] = rw[j];
     }
-    if (LVG_PANEL_PRIO) __builtin_amdgcn_s_setprio(0);
     __syncthreads();
     TACC(PH_P_WB, tpw);
 }
 
-// Single-wave panel (LVG_PANEL_W1): wave 0 factors the chunk alone, NMAX/64 rows per
-// lane in registers (physical rows ln, ln+64, ...). Per column: a compare over the
-// lane's rows, one DPP wave reduction (+ ballot) for the pivot and a v_readlane
-// broadcast of the pivot row; no workgroup barrier and no LDS round trip. Same
-// pivots (largest |v|, ties to the smallest logical position) and the same fma
-// sequence as panel_factor, so the factors are identical. Waves 1-3 go straight to
-// the closing barrier and leave their SIMDs to the co-resident workgroup.
-// R = 1 (the product path): when every row still active in the chunk lies in one
-// wave's tile rows (block columns c0 >= 64 * ((N - 1) / 64)), that wave factors the
-// chunk alone with its own rows. R = 4 (LVG_PANEL_W1, measured slower: the rows spill)
-// covers all rows from wave 0.
+// One-wave panel: when every row still active in the chunk lies in one or two waves'
+// tile rows (block columns c0 >= 128 at N = 256), wave w0 factors the chunk alone, R
+// rows per lane in registers. Per column: a compare over the lane's rows, one DPP wave
+// reduction (+ ballot) for the pivot and a v_readlane broadcast of the pivot row; no
+// workgroup barrier and no LDS round trip. Same pivots (largest |v|, ties to the
+// smallest logical position) and the same fma sequence as panel_factor, so the factors
+// are identical. The other waves go straight to the closing barrier and leave their
+// SIMDs to the co-resident workgroup.
 template <int R>
 __device__ __forceinline__ void panel_factor_wave(double *A, int N, int kk, int nb, double *b, Smem &sm, int w0,
                                                   const int (&rows)[R]) {
     if ((__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6) == w0) {
-        if (LVG_PANEL_PRIO) __builtin_amdgcn_s_setprio(2);
         const int ln = threadIdx.x & 63;
         double rw[R][NB], rb[R];
         bool act[R], part[R];
@@ -920,18 +357,13 @@ __device__ __forceinline__ void panel_factor_wave(double *A, int N, int kk, int 
 #pragma clang loop unroll(full)
         for (int c = 0; c < NB; c++) {
             if (c < nb) {
-                // the lane's best row: largest |v| (bit pattern; active rows flagged in
-                // the top bit), ties to the smallest logical position
+                // the lane's best row: largest key, ties to the smallest logical position
                 unsigned bh = 0u, bl = 0u;
                 int bp = 0x7fffffff, bs = 0;
 #pragma unroll
                 for (int i = 0; i < R; i++) {
-                    const double av = fabs(rw[i][c]);
-                    const unsigned long long bits =
-                        (act[i] && av == av) ? (unsigned long long)__double_as_longlong(av) : 0ull;
-                    const bool dnan = act[i] && lp[i] == c && av != av;   // NaN diagonal wins (oracle rule)
-                    const unsigned hi = dnan ? 0xffffffffu : act[i] ? ((unsigned)(bits >> 32) | 0x80000000u) : 0u;
-                    const unsigned lo = dnan ? 0xffffffffu : (unsigned)bits;
+                    unsigned hi, lo;
+                    pivot_key(rw[i][c], act[i], lp[i] == c, hi, lo);
                     const bool better = hi > bh || (hi == bh && (lo > bl || (lo == bl && (unsigned)lp[i] < (unsigned)bp)));
                     bh = better ? hi : bh;
                     bl = better ? lo : bl;
@@ -958,9 +390,7 @@ __device__ __forceinline__ void panel_factor_wave(double *A, int N, int kk, int 
                     bc = readlane_d(rbv, pl);
                 };
                 if (R == 1 || s == 0) bcast(rw[0], rb[0]);
-                else if (R == 2 || s == 1) bcast(rw[R > 1 ? 1 : 0], rb[R > 1 ? 1 : 0]);
-                else if (R == 3 || s == 2) bcast(rw[R > 2 ? 2 : 0], rb[R > 2 ? 2 : 0]);
-                else bcast(rw[R > 3 ? 3 : 0], rb[R > 3 ? 3 : 0]);
+                else bcast(rw[R > 1 ? 1 : 0], rb[R > 1 ? 1 : 0]);
                 const double piv = prow[c];
 #pragma unroll
                 for (int i = 0; i < R; i++) {
@@ -995,13 +425,12 @@ __device__ __forceinline__ void panel_factor_wave(double *A, int N, int kk, int 
                 for (int j = 0; j < NB; j++) sm.pu.P[p][j] = rw[i][j];
             }
         }
-        if (LVG_PANEL_PRIO) __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();
 }
 
 // ---- back substitution U x = y in logical order, blocked by NB from the bottom:
-//      wave 0 solves the diagonal block through LDS, then all threads update the
+//      wave 0 solves the diagonal block in registers, then all threads update the
 //      rows above; every entry receives its updates for k descending (oracle order).
 //      b: LDS [N] by physical row; on return sm.blog holds x (logical = level order).
 __device__ __forceinline__ void back_substitute(const double *A, int N, const double *b, Smem &sm) {
@@ -1079,26 +508,9 @@ __device__ __forceinline__ void back_substitute(const double *A, int N, const do
 
 __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Smem &sm, const LuSrc &src, const bool FUSED) {
     const int t = threadIdx.x;
-    // U values of the last TRSM, stored to A (for the back substitution only) behind the
-    // next step's loads: vmcnt counts loads and stores in order
-    double ux[TC / 2];
-    int64_t uo[TC / 2];
-#pragma unroll
-    for (int q = 0; q < TC / 2; q++) uo[q] = -1;
-    auto flush_u = [&]() {
-#pragma unroll
-        for (int q = 0; q < TC / 2; q++) {
-            if (uo[q] >= 0) A[uo[q]] = ux[q];
-            uo[q] = -1;
-        }
-    };
     const int rg = t >> 3, cg = t & 7;   // tile rows TR*rg.., columns TC*cg..
     double s_acc = (t == 0) ? 1. : 0.;             // residual row t (FUSED)
     for (int i = t; i < N; i += BT) { sm.perm[i] = i; sm.pos[i] = i; }
-    // L2 prefetch tokens: one dword per 128-byte line of the slot's operands read
-    // next (the next block column of K/li or A, the next chunk of L), so the loads
-    // that need them later hit L2 instead of HBM. Each token is consumed (waited on)
-    // only when the next prefetch of its kind is issued, long after it has landed.
     __syncthreads();
     for (int c0 = 0; c0 < N; c0 += WB) {
         TSTAMP(tp0);
@@ -1112,7 +524,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
 #pragma unroll
         for (int i = 0; i < TR; i++) prow[i] = (TR * rg + i < N) ? sm.perm[TR * rg + i] : 0;
         const int trow = (t < N) ? sm.perm[t] : 0;   // physical row of tile row t (L staging)
-        if (LVG_PANEL_ONEWAVE >= 2 && t < N) sm.tmap[t] = trow;
+        if (t < N) sm.tmap[t] = trow;
         // ---- block column c0..c0+wJ-1 into registers (physical rows, coalesced)
         if (!FUSED && src.BK) {
 #pragma unroll
@@ -1145,18 +557,11 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                 for (int i = 0; i < TR; i++) {
                     const bool ok = TR * rg + i < N;
                     const int64_t o = (int64_t)(ok ? prow[i] : 0) * N + c0 + TC * cg;
-                    if constexpr (TC == 4) {
-                        const double2 k0 = ok ? reinterpret_cast<const double2 *>(src.K + o)[0] : make_double2(0., 0.);
-                        const double2 k1 = ok ? reinterpret_cast<const double2 *>(src.K + o)[1] : make_double2(0., 0.);
-                        const int4 l4 = ok ? *reinterpret_cast<const int4 *>(src.li + o) : make_int4(-1, -1, -1, -1);
-                        acc[i][0] = k0.x; acc[i][1] = k0.y; acc[i][2] = k1.x; acc[i][3] = k1.y;
-                        li[i][0] = l4.x; li[i][1] = l4.y; li[i][2] = l4.z; li[i][3] = l4.w;
-                    } else {
-                        const double2 k0 = ok ? reinterpret_cast<const double2 *>(src.K + o)[0] : make_double2(0., 0.);
-                        const int2 l2 = ok ? *reinterpret_cast<const int2 *>(src.li + o) : make_int2(-1, -1);
-                        acc[i][0] = k0.x; acc[i][1] = k0.y;
-                        li[i][0] = l2.x; li[i][1] = l2.y;
-                    }
+                    const double2 k0 = ok ? reinterpret_cast<const double2 *>(src.K + o)[0] : make_double2(0., 0.);
+                    const double2 k1 = ok ? reinterpret_cast<const double2 *>(src.K + o)[1] : make_double2(0., 0.);
+                    const int4 l4 = ok ? *reinterpret_cast<const int4 *>(src.li + o) : make_int4(-1, -1, -1, -1);
+                    acc[i][0] = k0.x; acc[i][1] = k0.y; acc[i][2] = k1.x; acc[i][3] = k1.y;
+                    li[i][0] = l4.x; li[i][1] = l4.y; li[i][2] = l4.z; li[i][3] = l4.w;
                 }
             } else {
 #pragma unroll
@@ -1199,41 +604,9 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             }
         }
         TACC(PH_BLOAD, tp0);
-        // L rows / L11 entry of the next earlier-block chunk, prefetched during the
-        // current chunk's update (their values are final once the earlier blocks are)
-        double lnext[NB], l11next = 0.;
-        bool have_next = false;
-        auto fetch_l = [&](int k2, double (&lr)[NB], double &l11) {
-            const int nb2 = min(NB, N - k2);
-            // tile row t is logical row t here (earlier pivots were final at the block
-            // load), so rows t >= k2 + nb2 are below the chunk (LVG_LA_TILE: no LDS
-            // lookup) and rows k2..k2+nb2-1 are its pivot rows, whose L part is L11
-            // (LVG_L11_ROWS: L11 from those rows instead of a separate load)
-            const bool la = LVG_L11_ROWS ? (t < N && t >= k2)
-                          : LVG_LA_TILE ? (t < N && t >= k2 + nb2) : (t < N && sm.pos[trow] >= k2 + nb2);
-            const double *src_l = A + (int64_t)(la ? trow : 0) * N + k2;
-            if ((N & 1) == 0 && nb2 == NB) {
-                // 16-byte aligned row segment (N even, k2 a multiple of 16): 8 vector loads
-                const double2 *s2 = reinterpret_cast<const double2 *>(src_l);
-#pragma unroll
-                for (int m = 0; m < NB / 2; m++) {
-                    const double2 v = la ? s2[m] : make_double2(0., 0.);
-                    lr[2 * m] = v.x;
-                    lr[2 * m + 1] = v.y;
-                }
-            } else {
-#pragma unroll
-                for (int m = 0; m < NB; m++) lr[m] = (la && m < nb2) ? src_l[m] : 0.;
-            }
-            l11 = 0.;
-            if (!LVG_L11_ROWS) {
-                const int r = t / NB, m = t - r * NB;
-                l11 = (t < NB * NB && r < nb2 && m < r) ? A[(int64_t)sm.perm[k2 + r] * N + k2 + m] : 0.;
-            }
-        };
         for (int kk = 0; kk < c0 + wJ; kk += NB) {
             const int nb = min(NB, N - kk);
-            const int ub = LVG_UB2 ? (kk >> 4) & 1 : 0;   // Ub buffer of this chunk
+            const int ub = (kk >> 4) & 1;              // Ub buffer of this chunk
             int jlo;                                   // first block-local column to update
             if (kk >= c0) {
                 // ---- a chunk of this block column: all updates from k < kk are in; factor it
@@ -1247,22 +620,12 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                     }
                 }
                 __syncthreads();
-                if (LVG_PANEL_W1) {
-                    const int r4[4] = {t < N ? t : -1, t + 64 < N ? t + 64 : -1, t + 128 < N ? t + 128 : -1,
-                                       t + 192 < N ? t + 192 : -1};
-                    panel_factor_wave<4>(A, N, kk, nb, b, sm, 0, r4);
-                } else if (LVG_PANEL_ONEWAVE >= 3 && c0 >= 64 && (c0 >> 7) != ((N - 1) >> 7) && ((N - 1) >> 6) == 3) {
-                    // active rows in tile rows 64..255: one wave takes three rows per lane
-                    const int l = t & 63;
-                    const int r3[3] = {64 + l < N ? sm.tmap[64 + l] : -1, 128 + l < N ? sm.tmap[128 + l] : -1,
-                                       192 + l < N ? sm.tmap[192 + l] : -1};
-                    panel_factor_wave<3>(A, N, kk, nb, b, sm, 1, r3);
-                } else if (LVG_PANEL_ONEWAVE >= 2 && (c0 >> 6) != ((N - 1) >> 6) && (c0 >> 7) == ((N - 1) >> 7)) {
+                if ((c0 >> 6) != ((N - 1) >> 6) && (c0 >> 7) == ((N - 1) >> 7)) {
                     // active rows within two waves' tile rows: one wave takes both (2 rows per lane)
                     const int base = (c0 >> 7) << 7, l = t & 63;
                     const int r2[2] = {base + l < N ? sm.tmap[base + l] : -1, base + 64 + l < N ? sm.tmap[base + 64 + l] : -1};
                     panel_factor_wave<2>(A, N, kk, nb, b, sm, base >> 6, r2);
-                } else if (LVG_PANEL_ONEWAVE && (c0 >> 6) == ((N - 1) >> 6)) {
+                } else if ((c0 >> 6) == ((N - 1) >> 6)) {
                     // every active row is a tile row >= c0, all in wave c0 / 64: no barriers
                     const int r1[1] = {t < N ? trow : -1};
                     panel_factor_wave<1>(A, N, kk, nb, b, sm, c0 >> 6, r1);
@@ -1281,26 +644,37 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                 jlo = 0;
             }
             // L rows of chunk kk (rows below it) and, for an earlier block's chunk, its
-            // L11 entries: from A, prefetched during the previous step when possible;
-            // for a chunk of this block, from the panel output still in LDS (P). They
-            // land in LDS (LT, which aliases P) after the barrier below.
+            // L11 entries: from A for an earlier block's chunk; for a chunk of this block,
+            // from the panel output still in LDS (P). They land in LDS (LT, which aliases
+            // P) after the barrier below.
             static_assert(NB * NB <= BT, "one L11 entry per thread");
             double l11v = 0., lrow[NB];
             TSTAMP(tp2);
             if (kk < c0) {
-                if (have_next) {
+                // tile row t is logical row t here (earlier pivots were final at the block
+                // load), so rows t >= kk + nb are below the chunk
+                const bool la = t < N && t >= kk + nb;
+                const double *src_l = A + (int64_t)(la ? trow : 0) * N + kk;
+                if ((N & 1) == 0 && nb == NB) {
+                    // 16-byte aligned row segment (N even, kk a multiple of 16): 8 vector loads
+                    const double2 *s2 = reinterpret_cast<const double2 *>(src_l);
 #pragma unroll
-                    for (int m = 0; m < NB; m++) lrow[m] = lnext[m];
-                    l11v = l11next;
+                    for (int m = 0; m < NB / 2; m++) {
+                        const double2 v = la ? s2[m] : make_double2(0., 0.);
+                        lrow[2 * m] = v.x;
+                        lrow[2 * m + 1] = v.y;
+                    }
                 } else {
-                    fetch_l(kk, lrow, l11v);
+#pragma unroll
+                    for (int m = 0; m < NB; m++) lrow[m] = (la && m < nb) ? src_l[m] : 0.;
                 }
+                const int r = t / NB, m = t - r * NB;
+                l11v = (t < NB * NB && r < nb && m < r) ? A[(int64_t)sm.perm[kk + r] * N + kk + m] : 0.;
             } else {
                 const bool la = t < N && sm.pos[trow] >= kk + nb;
 #pragma unroll
                 for (int m = 0; m < NB; m++) lrow[m] = (la && m < nb) ? sm.pu.P[la ? trow : 0][m] : 0.;
             }
-            if (LVG_U_DEFER) flush_u();
             // ---- pivot rows of chunk kk (logical kk..kk+nb-1): their current values
             //      in this block column -> Ub (owners write from registers). For an
             //      earlier block's chunk they are tile rows kk.. (logical order as of
@@ -1315,17 +689,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                     }
                 }
             }
-            if (kk < c0) {
-                if (LVG_L11_ROWS) {
-                    if (t >= kk && t < kk + NB) {      // pivot row t - kk: its L part -> L11, stages l = 0
-                        const int r = t - kk;
-#pragma unroll
-                        for (int m = 0; m < NB; m++) { sm.L11[r][m] = (m < r) ? lrow[m] : 0.; lrow[m] = 0.; }
-                    }
-                } else if (t < NB * NB) {
-                    sm.L11[t / NB][t % NB] = l11v;
-                }
-            }
+            if (kk < c0 && t < NB * NB) sm.L11[t / NB][t % NB] = l11v;
             __syncthreads();
             TACC(PH_T_FETCH, tp2);
             TSTAMP(tp2s);
@@ -1358,14 +722,13 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                 LVG_TRSM_STEP(12) LVG_TRSM_STEP(13) LVG_TRSM_STEP(14)
 #undef LVG_TRSM_STEP
                 if (r < nb) {
-                    const int64_t prow = (int64_t)sm.perm[kk + r] * N + c0;
+                    const int64_t prw = (int64_t)sm.perm[kk + r] * N + c0;
 #pragma unroll
                     for (int q = 0; q < TC / 2; q++) {
                         const int c = (WB / 4) * w + (l >> 4) + 4 * q;
                         if (c >= jlo && c < wJ) {
                             sm.Ub[ub][r][c] = x[q];
-                            if (LVG_U_DEFER) { uo[q] = prow + c; ux[q] = x[q]; }
-                            else A[prow + c] = x[q];
+                            A[prw + c] = x[q];
                         }
                     }
                 }
@@ -1379,8 +742,6 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             }
             __syncthreads();
             TACC(PH_T_STAGE, tp2t);
-            have_next = LVG_PREFETCH_L && kk + NB < c0;
-            if (have_next) fetch_l(kk + NB, lnext, l11next);
             TACC(PH_TRSM, tp2);
             TSTAMP(tp3);
             // ---- rank-nb update of the rows below (8 x TC register tiles). No masks:
@@ -1395,54 +756,27 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                 for (int i = 0; i < TR; i++) any = any || (TR * rg + i < N && sm.pos[prow[i]] >= kk + nb);
             }
             if (any && TC * cg + TC - 1 >= jlo) {
-                // operands of step m+1 are read from LDS while step m computes
-                double a0[TR], u0[TC], a1[TR], u1[TC];
-                auto ld = [&](int m, double (&a)[TR], double (&u)[TC]) {
-                    if (LVG_GEMM_B128) {
-                        // 16-byte LDS reads (ds_read_b128: half the LDS cycles of ds_read2_b64)
-                        const double2 *ap = reinterpret_cast<const double2 *>(&sm.pu.LT[m][TR * rg]);
-                        const double2 *up = reinterpret_cast<const double2 *>(&sm.Ub[ub][m][TC * cg]);
+                for (int m = 0; m < nb; m++) {
+                    // 16-byte LDS reads (ds_read_b128: half the LDS cycles of ds_read2_b64)
+                    double a[TR], u[TC];
+                    const double2 *ap = reinterpret_cast<const double2 *>(&sm.pu.LT[m][TR * rg]);
+                    const double2 *up = reinterpret_cast<const double2 *>(&sm.Ub[ub][m][TC * cg]);
 #pragma unroll
-                        for (int i = 0; i < TR / 2; i++) { const double2 v = ap[i]; a[2 * i] = v.x; a[2 * i + 1] = v.y; }
+                    for (int i = 0; i < TR / 2; i++) { const double2 v = ap[i]; a[2 * i] = v.x; a[2 * i + 1] = v.y; }
 #pragma unroll
-                        for (int j = 0; j < TC / 2; j++) { const double2 v = up[j]; u[2 * j] = v.x; u[2 * j + 1] = v.y; }
-                    } else {
-#pragma unroll
-                        for (int i = 0; i < TR; i++) a[i] = sm.pu.LT[m][TR * rg + i];
-#pragma unroll
-                        for (int j = 0; j < TC; j++) u[j] = sm.Ub[ub][m][TC * cg + j];
-                    }
-                };
-                auto upd = [&](const double (&a)[TR], const double (&u)[TC]) {
+                    for (int j = 0; j < TC / 2; j++) { const double2 v = up[j]; u[2 * j] = v.x; u[2 * j + 1] = v.y; }
 #pragma unroll
                     for (int i = 0; i < TR; i++)
 #pragma unroll
                         for (int j = 0; j < TC; j++) acc[i][j] = fma(-a[i], u[j], acc[i][j]);
-                };
-                if (LVG_GEMM_PIPE) {
-                    ld(0, a0, u0);
-                    for (int m = 0; m < nb; m += 2) {
-                        if (m + 1 < nb) ld(m + 1, a1, u1);
-                        upd(a0, u0);
-                        if (m + 1 < nb) {
-                            if (m + 2 < nb) ld(m + 2, a0, u0);
-                            upd(a1, u1);
-                        }
-                    }
-                } else {
-                    for (int m = 0; m < nb; m++) { ld(m, a0, u0); upd(a0, u0); }
                 }
             }
             // between two earlier chunks the next step's opening barrier suffices: its Ub goes
             // to the other buffer, L11 and LT are only rewritten after every wave has left
             // this step's TRSM / passed that barrier
-            if (!(LVG_UB2 && kk + NB < c0)) __syncthreads();
+            if (kk + NB >= c0) __syncthreads();
             TACC(PH_GEMM, tp3);
         }
-    }
-    if (LVG_U_DEFER) {
-        flush_u();
-        __syncthreads();          // the back substitution reads U rows other threads stored
     }
     back_substitute(A, N, b, sm);
     double emax = 0.;
@@ -1450,25 +784,9 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
     return FUSED ? block_max(emax, sm) : 0.;
 }
 
-
 // ------------------------------------------------------------------------------
 // iteration_control (iteration_control.h:84-242)
 // ------------------------------------------------------------------------------
-struct Ctl {
-    int acceleration, accel_start, accel_period, nb_prev, max_iter;
-    int iter_nb, nb_after_accel;
-    double best_eq, eq_error, pop_error, rel_error;
-    int hp, np, hr, nr;   // ring heads and sizes: prev_level_pop / residual_list
-};
-
-struct Slot {
-    double *K, *A, *prev, *res, *opt, *y, *given, *df;
-};
-
-__device__ __forceinline__ double *ring(double *base, int head, int i, int N) {
-    return base + (int64_t)((head + i) & (NHIST - 1)) * N;
-}
-
 // accel_step (iteration_control.h:139-193). Each of the nb_param*nb_param + nb_param
 // sums runs in one thread in the reference's k order; the small system is solved
 // by thread 0 exactly as oracle_lu_solve does.
@@ -1492,37 +810,7 @@ __device__ __forceinline__ void accel_step(Ctl &C, Slot &S, int N, Smem &sm) {
         sm.pu.hist_acc[t] = a;
     }
     __syncthreads();
-    if (t == 0) {
-        double Am[4][4], bv[4];
-        for (int i = 0; i < np; i++) {
-            for (int j = 0; j < np; j++) Am[i][j] = sm.pu.hist_acc[i * np + j];
-            bv[i] = sm.pu.hist_acc[np * np + i];
-        }
-        for (int k = 0; k < np; k++) {
-            int p = k;
-            double amax = fabs(Am[k][k]);
-            for (int i = k + 1; i < np; i++) if (fabs(Am[i][k]) > amax) { amax = fabs(Am[i][k]); p = i; }
-            if (p != k) {
-                for (int j = 0; j < np; j++) { double x = Am[k][j]; Am[k][j] = Am[p][j]; Am[p][j] = x; }
-                double x = bv[k]; bv[k] = bv[p]; bv[p] = x;
-            }
-            double piv = Am[k][k];
-            for (int i = k + 1; i < np; i++) {
-                double l = Am[i][k] / piv;
-                Am[i][k] = l;
-                for (int j = k + 1; j < np; j++) Am[i][j] = fma(-l, Am[k][j], Am[i][j]);
-                bv[i] = fma(-l, bv[k], bv[i]);
-            }
-        }
-        for (int k = np - 1; k >= 0; k--) {
-            bv[k] /= Am[k][k];
-            double x = bv[k];
-            for (int i = 0; i < k; i++) bv[i] = fma(-Am[i][k], x, bv[i]);
-        }
-        double sum = 0.;
-        for (int i = 0; i < np; i++) { sum = sum + bv[i]; sm.pu.hist_acc[16 + i] = bv[i]; }
-        sm.pu.hist_acc[31] = sum;
-    }
+    if (t == 0) accel_solve_small(sm.pu.hist_acc, np);
     __syncthreads();
     const double sum = sm.pu.hist_acc[31];
     for (int k = t; k < N; k += BT) {
@@ -1532,11 +820,6 @@ __device__ __forceinline__ void accel_step(Ctl &C, Slot &S, int N, Smem &sm) {
     }
     __syncthreads();
 }
-
-// next_step (iteration_control.h:84-137)
-
-// calculate_populations (iteration_control.h:196-242); pops in/out in sm.pold
-
 
 // iteration_control::next_step (iteration_control.h:84-137), split around the
 // calc_new_pop solve so that the layer driver has a single LU call site.
@@ -1606,21 +889,6 @@ __device__ __forceinline__ void start_pass(Ctl &C, const LvgDevProblem &P, Slot 
     __syncthreads();
 }
 
-__device__ __forceinline__ Slot make_slot(const LvgDevProblem &P, const LvgLaunch &Lc, int slot) {
-    const int N = P.N;
-    double *w = Lc.ws + (int64_t)slot * Lc.ws_stride;
-    Slot S;
-    S.K = w; w += (int64_t)N * N;
-    S.A = w; w += (int64_t)N * N;
-    S.prev = w; w += (int64_t)NHIST * N;
-    S.res = w; w += (int64_t)NHIST * N;
-    S.opt = w; w += N;
-    S.given = w; w += N;
-    S.df = w; w += N;
-    S.y = w;
-    return S;
-}
-
 // One layer of calc_molecular_populations (radiative_transfer.cpp:236-288). from_prev:
 // warm chain and the previous layer of the chain converged (:247-249). Returns is_found.
 __device__ __forceinline__ bool solve_layer(const LvgDevProblem &P, const LvgLaunch &Lc, int l, Slot &S, Smem &sm,
@@ -1642,10 +910,9 @@ __device__ __forceinline__ bool solve_layer(const LvgDevProblem &P, const LvgLau
         if (need_boundary && !from_prev) {
             if (Lc.ball) Bsrc = Lc.ball + (int64_t)l * N * N;   // the boundary LU loads B from here
             else Bdg = Lc.bdiag + (int64_t)l * N;               // ... or forms it from K
-
         }
     } else {
-        build_collision_operators(P, sm, S.K, (need_boundary && !from_prev) ? S.A : nullptr);
+        layer_collisions(P, sm, S.K, (need_boundary && !from_prev) ? S.A : nullptr);
     }
     TACC(PH_SETUP, ts0);
 
@@ -1733,13 +1000,13 @@ __device__ __forceinline__ bool solve_layer(const LvgDevProblem &P, const LvgLau
 
 // Persistent: workgroups pull queue items (layers, or whole warm chains) from an atomic
 // counter; `order` maps queue positions to items (longest expected first).
-__global__ void __launch_bounds__(BT, LVG_OCC) solve_kernel(const LvgDevProblem *__restrict__ Pp,
-                                                       const LvgLaunch *__restrict__ Lp) {
+__global__ void __launch_bounds__(BT, OCC) solve_kernel(const LvgDevProblem *__restrict__ Pp,
+                                                        const LvgLaunch *__restrict__ Lp) {
     __shared__ Smem sm;
     const LvgDevProblem &P = *Pp;
     const LvgLaunch &Lc = *Lp;
     PH_INIT();
-    load_rule_table(P, sm);
+    load_rule_table<BT>(P, sm);
     Slot S = make_slot(P, Lc, blockIdx.x);
     const int nq = Lc.chain_off ? Lc.nb_chain : Lc.nb_lay;
     for (;;) {
@@ -1765,17 +1032,17 @@ __global__ void __launch_bounds__(BT, LVG_OCC) solve_kernel(const LvgDevProblem 
 }
 
 // lvg_debug_calc_new_pop: one calc_new_pop for one layer (block 0 only)
-__global__ void __launch_bounds__(BT, LVG_OCC) debug_kernel(const LvgDevProblem *__restrict__ Pp,
-                                                       const LvgLaunch *__restrict__ Lp) {
+__global__ void __launch_bounds__(BT, OCC) debug_kernel(const LvgDevProblem *__restrict__ Pp,
+                                                        const LvgLaunch *__restrict__ Lp) {
     __shared__ Smem sm;
     const LvgDevProblem &P = *Pp;
     const LvgLaunch &Lc = *Lp;
-    load_rule_table(P, sm);
+    load_rule_table<BT>(P, sm);
     Slot S = make_slot(P, Lc, 0);
     const int N = P.N, t = threadIdx.x;
     const LvgModeLines &M = Lc.line_overlap ? P.overlap : P.plain;
     layer_setup(P, Lc, 0, sm);
-    build_collision_operators(P, sm, S.K, nullptr);
+    layer_collisions(P, sm, S.K, nullptr);
     for (int i = t; i < N; i += BT) sm.pold[i] = Lc.dbg_pop_in[i];
     __syncthreads();
     double *yp = (2 * M.nb_lines <= YCAP) ? sm.ylds : S.y;   // line terms in LDS when they fit
@@ -1797,14 +1064,14 @@ __global__ void __launch_bounds__(BT, LVG_OCC) debug_kernel(const LvgDevProblem 
 // with the first layer's populations, as the reference, or the layer's own), then the
 // neutral collision rates j -> i for every i (coll_rates.cpp:225-240) in level order,
 // read from the neutral-only collision operator K_n (rate j -> i = K_n[i][j]).
-__global__ void __launch_bounds__(BT, LVG_OCC) lum_kernel(const LvgDevProblem *__restrict__ Pp,
-                                                     const LvgLaunch *__restrict__ Lp,
-                                                     const LvgLumArgs *__restrict__ Ap) {
+__global__ void __launch_bounds__(BT, OCC) lum_kernel(const LvgDevProblem *__restrict__ Pp,
+                                                      const LvgLaunch *__restrict__ Lp,
+                                                      const LvgLumArgs *__restrict__ Ap) {
     __shared__ Smem sm;
     const LvgDevProblem &P = *Pp;
     const LvgLaunch &Lc = *Lp;
     const LvgLumArgs &A = *Ap;
-    load_rule_table(P, sm);
+    load_rule_table<BT>(P, sm);
     Slot S = make_slot(P, Lc, blockIdx.x);
     const LvgModeLines &M = P.plain;
     const int N = P.N, t = threadIdx.x, T = A.nb_trans, nl = Lc.nb_lay;
@@ -1816,7 +1083,7 @@ __global__ void __launch_bounds__(BT, LVG_OCC) lum_kernel(const LvgDevProblem *_
         __syncthreads();
         if (l >= nl) break;
         layer_setup(P, Lc, l, sm);
-        build_collision_operators(P, sm, S.K, nullptr, false);
+        layer_collisions(P, sm, S.K, nullptr, false);
         const double *pl = Lc.pops + (int64_t)l * N;
         const double *ip = A.layer_pops ? pl : Lc.pops;
         for (int w = t; w < 2 * T; w += BT) {
@@ -1873,8 +1140,6 @@ __global__ void __launch_bounds__(64) lum_reduce_kernel(const LvgLumArgs *__rest
 }
 
 #if !LVG_BIG
-#include "lvg_wave.h"
-
 // ---- collision operators of a whole batch of layers, ahead of the solve ----------------
 // build_collision_operators for every layer of the launch into K_all / B_all (HBM), with
 // a small LDS footprint (layer scalars and the rule table only) so that many workgroups
@@ -1894,22 +1159,17 @@ struct CollSmem {
     int8_t ttab[LVG_MAX_CLASSES][LVG_MAX_TERMS], tcombo[LVG_MAX_CLASSES][LVG_MAX_TERMS];
     int8_t tet[LVG_MAX_CLASSES], tgrp[LVG_MAX_CLASSES];
     double dust[LVG_MAX_DUST];
-    union { double d[1]; } pu;          // too small to stage pair classes: they come from HBM
 };
 
-#ifndef LVG_COLL_K_PU
-#define LVG_COLL_K_PU 2               // pair tiles per batch in coll_kernel (1 and 8 WG/CU variants spill)
-#endif
-#ifndef LVG_COLL_K_OCC
-#define LVG_COLL_K_OCC 4              // workgroups per CU coll_kernel is built for (register budget)
-#endif
-__global__ void __launch_bounds__(BT, LVG_COLL_K_OCC) coll_kernel(const LvgDevProblem *__restrict__ Pp,
-                                                                  const LvgLaunch *__restrict__ Lp) {
+constexpr int COLL_K_PU = 2;    // pair tiles per batch in coll_kernel (1 and 8 WG/CU variants spill)
+constexpr int COLL_K_OCC = 4;   // workgroups per CU coll_kernel is built for (register budget)
+__global__ void __launch_bounds__(BT, COLL_K_OCC) coll_kernel(const LvgDevProblem *__restrict__ Pp,
+                                                              const LvgLaunch *__restrict__ Lp) {
     __shared__ CollSmem sm;
     const LvgDevProblem &P = *Pp;
     const LvgLaunch &Lc = *Lp;
     PH_INIT();
-    load_rule_table(P, sm);
+    load_rule_table<BT>(P, sm);
     const int64_t NN = (int64_t)P.N * P.N;
     // XCD-aware: workgroups are dispatched round-robin over the 8 XCDs, so workgroup b
     // takes position chunk (b % 8) of the temperature-ordered list: each XCD's resident
@@ -1921,7 +1181,8 @@ __global__ void __launch_bounds__(BT, LVG_COLL_K_OCC) coll_kernel(const LvgDevPr
         if (threadIdx.x == 0) layer_scalars(P, Lc, l, sm);
         __syncthreads();
         double *Kl = const_cast<double *>(Lc.kall) + l * NN;
-        build_collision_operators<CollSmem, LVG_COLL_K_PU>(P, sm, Kl, Lc.ball ? const_cast<double *>(Lc.ball) + l * NN : nullptr);
+        build_collision_operators<BT, COLL_K_PU>(P, sm, Kl, Lc.ball ? const_cast<double *>(Lc.ball) + l * NN : nullptr,
+                                                 nullptr);
         if (Lc.bdiag) {
             // B's diagonal only (no electron rates: B = K + A/2 above the diagonal, K below):
             // minus the ascending column sum, as build_collision_operators forms it
@@ -1931,8 +1192,8 @@ __global__ void __launch_bounds__(BT, LVG_COLL_K_OCC) coll_kernel(const LvgDevPr
                 for (int r = 0; r < N; r++) {
                     if (r == d) continue;
                     const double k = Kl[(int64_t)r * N + d];
-                    const double b = (r < d) ? 0.5 * P.einst[(int64_t)d * N + r] + k : k;
-                    a = a - b;
+                    const double bb = (r < d) ? 0.5 * P.einst[(int64_t)d * N + r] + k : k;
+                    a = a - bb;
                 }
                 const_cast<double *>(Lc.bdiag)[(int64_t)l * N + d] = a;
             }
@@ -1946,10 +1207,9 @@ __global__ void __launch_bounds__(BT, LVG_COLL_K_OCC) coll_kernel(const LvgDevPr
 }  // namespace LVG_NS
 
 extern "C" hipError_t LVG_SYM(lvg_launch_lum)(const LvgDevProblem *P, const LvgLaunch *L, const LvgLumArgs *A, int grid,
-                                     int nb_trans, int nb_lay, hipStream_t s) {
+                                              int nb_trans, int nb_lay, hipStream_t s) {
     hipLaunchKernelGGL(LVG_NS::lum_kernel, dim3(grid), dim3(LVG_NS::BT), 0, s, P, L, A);
     hipLaunchKernelGGL(LVG_NS::lum_reduce_kernel, dim3((nb_trans + 63) / 64), dim3(64), 0, s, A, nb_lay);
-    (void)nb_lay;
     return hipGetLastError();
 }
 
@@ -1970,48 +1230,6 @@ extern "C" hipError_t LVG_SYM(lvg_launch_debug)(const LvgDevProblem *P, const Lv
     hipLaunchKernelGGL(LVG_NS::debug_kernel, dim3(1), dim3(LVG_NS::BT), 0, s, P, L);
     return hipGetLastError();
 }
-
-#if !LVG_BIG
-// ---- wave-per-layer kernel (lvg_wave.h) for N <= 64 ----------------------------------
-// 1 and the waves per block / dynamic LDS bytes if it applies to N levels with
-// nb_y line terms and grid_doubles escape-grid points; 0 if not.
-extern "C" int lvg_wave_plan(int N, int nb_y, int grid_doubles, size_t lds_cap, int *wpb, size_t *dyn) {
-    if (N < 2 || N > lvg::WNMAX || nb_y > lvg::WYCAP || grid_doubles > lvg::WGRID_CAP) return 0;
-    for (int w = 4; w >= 1; w >>= 1) {
-        const size_t d = lvg::wave_dyn_bytes(N, w);
-        if (sizeof(lvg::WaveShared) + d <= lds_cap) { *wpb = w; *dyn = d; return 1; }
-    }
-    return 0;
-}
-
-// instantiations every 8 levels from 24 up (the unrolled row loops run to NM): OH-HF 24
-// and p-H2O 45 run NM = 24 and 48, the reference's OH-HF 56 runs NM = 56
-#define LVG_WAVE_NMS(X) X(16) X(24) X(32) X(40) X(48) X(56) X(64)
-static int wave_nm(int N) { return N <= 16 ? 16 : ((N + 7) / 8) * 8; }
-static const void *wave_kernel(int N) {
-#define LVG_WK(NM_) if (wave_nm(N) == NM_) return reinterpret_cast<const void *>(&lvg::solve_wave_kernel<NM_>);
-    LVG_WAVE_NMS(LVG_WK)
-#undef LVG_WK
-    return nullptr;
-}
-
-extern "C" hipError_t lvg_wave_occupancy(int N, int wpb, size_t dyn, int *blocks_per_cu) {
-    const void *k = wave_kernel(N);
-    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
-    if (e != hipSuccess) return e;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 64 * wpb, dyn);
-}
-
-extern "C" hipError_t lvg_launch_solve_wave(const LvgDevProblem *P, const LvgLaunch *L, int N, int grid, int wpb,
-                                            size_t dyn, hipStream_t s) {
-    const dim3 g(grid), b(64 * wpb);
-#define LVG_WL(NM_) if (wave_nm(N) == NM_) hipLaunchKernelGGL(lvg::solve_wave_kernel<NM_>, g, b, dyn, s, P, L);
-    LVG_WAVE_NMS(LVG_WL)
-#undef LVG_WL
-    return hipGetLastError();
-}
-extern "C" size_t lvg_wave_static_lds(void) { return sizeof(lvg::WaveShared); }
-#endif
 
 extern "C" int LVG_SYM(lvg_kernel_max_levels)(void) { return LVG_NS::NMAX; }
 extern "C" int LVG_SYM(lvg_kernel_block_threads)(void) { return LVG_NS::BT; }

@@ -1,6 +1,4 @@
-// lvg_wave.h — wave-per-layer solver for small molecules (N <= 64), included by
-// lvg_kernels.hip inside namespace lvg (it reuses the block kernel's layer scalars,
-// line-term and iteration-control helpers).
+// lvg_wave.hip — wave-per-layer solver for small molecules (N <= 64).
 //
 // Why a second kernel: for N <= 64 the 256-thread block of solve_kernel keeps at most
 // N threads busy and pays a workgroup barrier per LU column (ph2o45: ≈2 K cycles a
@@ -17,30 +15,31 @@
 //    same atomic queue as solve_kernel.
 // The arithmetic of every step is the block kernel's (and the oracle's), in the same
 // order; results are bit-identical, which tests/test_gpu_parity.py checks.
-#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
 
-#ifndef LVG_WAVE_CLAMP
-#define LVG_WAVE_CLAMP 1              // assembly operands read unconditionally (clamped indices)
+#include "lvg_device.h"
+#include "../../include/lvg_amd.h"
+#include "../../include/lvg_math.h"
+
+namespace lvg {
+
+#include "lvg_common.h"
+
+#ifdef LVG_PHASE_TIMERS
+// timer build: every wave's lane 0 accumulates (LDS atomics), not just thread 0 of the block
+#undef TACC
+#define TACC(ph, v0) do { if ((threadIdx.x & 63) == 0) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    atomicAdd(&lvg_ph_lds[ph], t_ - (v0)); } } while (0)
 #endif
-#ifndef LVG_WAVE_OPAQUE_N
-#define LVG_WAVE_OPAQUE_N 1
-#endif
-#ifndef LVG_WAVE_LINE_INV
-#define LVG_WAVE_LINE_INV 1           // line terms from per-layer invariant records (wave_line_invariants)
-#endif
-#ifndef LVG_WAVE_KROW
-#define LVG_WAVE_KROW 1               // 1: the lane's K / line-index row held in registers for the layer
-#endif
-#ifndef LVG_WAVE_ACCEL_BATCH
-#define LVG_WAVE_ACCEL_BATCH 1        // Ng sums: ring reads of 8 levels per round trip
-#endif
+
 constexpr int WYCAP = 512;        // line terms y per wave kept in LDS (host checks 2*nb_lines <= WYCAP)
 constexpr int WGRID_CAP = 1024;   // escape + overlap grid doubles copied to LDS (host checks)
-constexpr int WNMAX = 64;
+constexpr int WNMAX = LVG_WAVE_NMAX;
 
 struct WaveLayer {                // per-wave LDS
     double pold[WNMAX], pnew[WNMAX], diag[WNMAX];
-    alignas(16) double prow[WNMAX + 2];   // LU: the pivot row of the current column, then its b
     double y[WYCAP];
     double hist_acc[32];
     double T, Te, vw, vgrad, nmol, ne;
@@ -54,13 +53,6 @@ struct WaveLayer {                // per-wave LDS
     double tx[LVG_MAX_TABLES];
     double dust[LVG_MAX_DUST];
 };
-
-#ifdef LVG_PHASE_TIMERS
-// timer build: every wave's lane 0 accumulates (LDS atomics), not just thread 0 of the block
-#undef TACC
-#define TACC(ph, v0) do { if ((threadIdx.x & 63) == 0) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-    atomicAdd(&lvg_ph_lds[ph], t_ - (v0)); } } while (0)
-#endif
 
 struct WaveShared {               // per-block LDS (static part)
     int8_t ttab[LVG_MAX_CLASSES][LVG_MAX_TERMS], tcombo[LVG_MAX_CLASSES][LVG_MAX_TERMS];
@@ -140,7 +132,7 @@ __device__ __forceinline__ void wave_collisions(const LvgDevProblem &P, const Wa
 
 // ---- line terms with the table lookups batched -------------------------------------
 // Same arithmetic as esc_func / overlap_esc_func / intensity_single / intensity_pair
-// (lvg_kernels.hip), reorganised so that a lane's independent table reads are issued
+// (lvg_common.h), reorganised so that a lane's independent table reads are issued
 // together: the bisections run in LDS first, then every table value the lane needs
 // is loaded in one round trip. Overlap: the p1 and p2 tables share the interpolation
 // indices (same gamma, delta, gratio, dx), so each direction is located once.
@@ -148,28 +140,6 @@ struct OvIdx {
     int m, n, k, l;
     double y, p, u, t;
 };
-__device__ __forceinline__ OvIdx ov_index(const LvgDevProblem &P, const EscGrids &G, double gamma, double ldelta,
-                                          double gratio, double dxv) {
-    OvIdx o;
-    o.m = locate_index(G.old, P.ov_nd, ldelta);
-    o.l = locate_index(G.og, P.ov_ng, gamma);
-    o.k = locate_index(G.ogr, P.ov_ngr, gratio);
-    o.n = locate_index(G.odx, P.ov_ndx, dxv);
-    o.y = 0.; o.u = 0.; o.t = 0.; o.p = 0.;
-    if (o.m < 0) o.m = 0;
-    else if (o.m > P.ov_nd - 2) { o.m = P.ov_nd - 2; o.y = 1.; }
-    else o.y = (ldelta - G.old[o.m]) / (G.old[o.m + 1] - G.old[o.m]);
-    if (o.n < 0) o.n = 0;
-    else if (o.n > P.ov_ndx - 2) { o.p = 1.; o.n = P.ov_ndx - 2; }
-    else o.p = (dxv - G.odx[o.n]) / (G.odx[o.n + 1] - G.odx[o.n]);
-    if (o.l < 0) o.l = 0;
-    else if (o.l > P.ov_ng - 2) { o.l = P.ov_ng - 2; o.u = 1.; }
-    else o.u = (gamma - G.og[o.l]) / (G.og[o.l + 1] - G.og[o.l]);
-    if (o.k < 0) o.k = 0;
-    else if (o.k > P.ov_ngr - 2) { o.t = 1.; o.k = P.ov_ngr - 2; }
-    else o.t = (gratio - G.ogr[o.k]) / (G.ogr[o.k + 1] - G.ogr[o.k]);
-    return o;
-}
 __device__ __forceinline__ void ov_load(const LvgDevProblem &P, const double *tab, const OvIdx &o, double (&v)[16]) {
     const int W = P.ov_ngr * P.ov_ng, ndx = P.ov_ndx, ng = P.ov_ng;
 #pragma unroll
@@ -202,19 +172,6 @@ struct EscIdx {
     int k, l;
     double t, u;
 };
-__device__ __forceinline__ EscIdx esc_index(const LvgDevProblem &P, const EscGrids &G, double gamma, double delta) {
-    const int nd = P.esc_nd, ng = P.esc_ng;
-    EscIdx o;
-    o.k = locate_index(G.ed, nd, delta);
-    o.l = locate_index(G.eg, ng, gamma);
-    if (o.k < 0) { o.t = 0.; o.k = 0; }
-    else if (o.k > nd - 2) { o.t = 1.; o.k = nd - 2; }
-    else o.t = (delta - G.ed[o.k]) / (G.ed[o.k + 1] - G.ed[o.k]);
-    if (o.l < 0) { o.l = 0; o.u = 0.; }
-    else if (o.l > ng - 2) { o.l = ng - 2; o.u = 1.; }
-    else o.u = (gamma - G.eg[o.l]) / (G.eg[o.l + 1] - G.eg[o.l]);
-    return o;
-}
 __device__ __forceinline__ void esc_load(const LvgDevProblem &P, const EscIdx &o, double (&v)[4]) {
     const int ng = P.esc_ng;
     const double *p = P.esc_p;
@@ -242,6 +199,7 @@ enum { WI_N1, WI_U1, WI_L1, WI_A1, WI_B1, WI_C, WI_EK, WI_ET, WI_PLAIN,
        WI_N2 = WI_PLAIN, WI_U2, WI_L2, WI_A2, WI_B2, WI_DX, WI_OM, WI_OY, WI_AN, WI_AP, WI_BN, WI_BP, WI_ALL };
 static_assert(WI_ALL == LVG_WAVE_INV_FIELDS, "host reserves LVG_WAVE_INV_FIELDS doubles per line");
 
+// locate_index + clamp to the interpolation interval (esc_func / overlap_esc_func)
 __device__ __forceinline__ void ov_interval(const double *g, int n, double x, int &j, double &w) {
     j = locate_index(g, n, x);
     if (j < 0) { j = 0; w = 0.; }
@@ -259,7 +217,7 @@ __device__ __forceinline__ void wave_line_invariants(const LvgDevProblem &P, con
         const int u1 = M.line_u[n1], l1 = M.line_l[n1];
         int k;
         double t;
-        ov_interval(G.ed, P.esc_nd, delta, k, t);   // esc_index's delta part
+        ov_interval(G.ed, P.esc_nd, delta, k, t);   // esc_func's delta part
         inv[WI_N1 * cap + q] = n1;
         inv[WI_U1 * cap + q] = u1;
         inv[WI_L1 * cap + q] = l1;
@@ -294,10 +252,10 @@ __device__ __forceinline__ void wave_line_invariants(const LvgDevProblem &P, con
     }
 }
 
-// plain scheme from the invariants: WUB units per lane per pass, stores last
-__device__ __forceinline__ void wave_line_terms_plain_inv(const LvgDevProblem &P, const EscGrids &G,
-                                                          const LvgModeLines &M, WaveLayer &sm, const double *inv,
-                                                          int cap) {
+// plain scheme from the invariants: B units per lane per pass, stores last
+__device__ __forceinline__ void wave_line_terms_plain(const LvgDevProblem &P, const EscGrids &G,
+                                                      const LvgModeLines &M, WaveLayer &sm, const double *inv,
+                                                      int cap) {
     const int t = lane_id(), U = M.nb_units;
     constexpr int B = 4;
     for (int q0 = t; q0 < U; q0 += 64 * B) {
@@ -319,7 +277,7 @@ __device__ __forceinline__ void wave_line_terms_plain_inv(const LvgDevProblem &P
             const double gamma = fabs(sm.vgrad) / (sm.vw * op[b]);
             ix[b].k = (int)f[b][WI_EK];
             ix[b].t = f[b][WI_ET];
-            ov_interval(G.eg, P.esc_ng, gamma, ix[b].l, ix[b].u);   // esc_index's gamma part
+            ov_interval(G.eg, P.esc_ng, gamma, ix[b].l, ix[b].u);   // esc_func's gamma part
         }
 #pragma unroll
         for (int b = 0; b < B; b++) esc_load(P, ix[b], tv[b]);
@@ -336,9 +294,9 @@ __device__ __forceinline__ void wave_line_terms_plain_inv(const LvgDevProblem &P
 }
 
 // overlap scheme from the invariants (intensity_single / intensity_pair sequences)
-__device__ __forceinline__ void wave_line_terms_overlap_inv(const LvgDevProblem &P, const EscGrids &G,
-                                                            const LvgModeLines &M, WaveLayer &sm, const double *inv,
-                                                            int cap) {
+__device__ __forceinline__ void wave_line_terms_overlap(const LvgDevProblem &P, const EscGrids &G,
+                                                        const LvgModeLines &M, WaveLayer &sm, const double *inv,
+                                                        int cap) {
     const double max_dx = 4.;
     const double *pop = sm.pold;
     for (int q = lane_id(); q < M.nb_units; q += 64) {
@@ -432,157 +390,23 @@ __device__ __forceinline__ void wave_line_terms_overlap_inv(const LvgDevProblem 
     }
 }
 
-// plain scheme: WUB single-line units per lane per pass (intensity_single), stores last
-constexpr int WUB = 4;
-__device__ __forceinline__ void wave_line_terms_plain(const LvgDevProblem &P, const EscGrids &G, const LvgModeLines &M,
-                                                      WaveLayer &sm) {
-    const int t = lane_id();
-    for (int q0 = t; q0 < M.nb_units; q0 += 64 * WUB) {
-        int n[WUB];
-        double I[WUB], aul[WUB], alu[WUB];
-        EscIdx ix[WUB];
-        double em[WUB], op[WUB], tv[WUB][4];
-#pragma unroll
-        for (int b = 0; b < WUB; b++) {
-            const int q = q0 + 64 * b;
-            n[b] = (q < M.nb_units) ? M.unit_l0[q] : M.unit_l0[t];
-        }
-#pragma unroll
-        for (int b = 0; b < WUB; b++) {
-            const int nn = n[b];
-            const int u = M.line_u[nn], l = M.line_l[nn];
-            const double energy = M.line_e[nn];
-            aul[b] = M.line_aul[nn];
-            alu[b] = M.line_alu[nn];
-            const double c = sm.nmol / (EIGHT_PI * sm.vw * energy * energy * energy);
-            em[b] = c * aul[b] * sm.pold[u];
-            op[b] = c * alu[b] * sm.pold[l] - em[b] + MIN_LINE_OPACITY;
-            if (op[b] < 0.) op[b] *= INV_TRANS_FACTOR;
-            const double dop = dust_opacity(P, M, sm, nn);
-            const double gamma = fabs(sm.vgrad) / (sm.vw * op[b]);
-            const double delta = fabs(sm.vgrad) / (sm.vw * dop);
-            ix[b] = esc_index(P, G, gamma, delta);
-        }
-#pragma unroll
-        for (int b = 0; b < WUB; b++) esc_load(P, ix[b], tv[b]);
-#pragma unroll
-        for (int b = 0; b < WUB; b++) I[b] = em[b] / op[b] * esc_sum(ix[b], tv[b]);
-#pragma unroll
-        for (int b = 0; b < WUB; b++) {
-            if (q0 + 64 * b < M.nb_units) {
-                sm.y[2 * n[b]] = aul[b] * (1. + I[b]);
-                sm.y[2 * n[b] + 1] = alu[b] * I[b];
-            }
-        }
-    }
-}
-
-// overlap scheme: one unit per lane per pass; pairs through intensity_pair's sequence
-__device__ __forceinline__ void wave_line_terms_overlap(const LvgDevProblem &P, const EscGrids &G,
-                                                        const LvgModeLines &M, WaveLayer &sm) {
-    const double max_dx = 4.;
-    for (int q = lane_id(); q < M.nb_units; q += 64) {
-        const int n1 = M.unit_l0[q], n2 = M.unit_l1[q];
-        if (n2 < 0) {
-            const double I = intensity_single(P, G, M, sm, n1, sm.pold);
-            sm.y[2 * n1] = M.line_aul[n1] * (1. + I);
-            sm.y[2 * n1 + 1] = M.line_alu[n1] * I;
-            continue;
-        }
-        const double *pop = sm.pold;
-        const int u1 = M.line_u[n1], l1 = M.line_l[n1], u2 = M.line_u[n2], l2 = M.line_l[n2];
-        const double energy = M.line_e[n1];
-        double c = sm.nmol / (EIGHT_PI * sm.vw * energy * energy * energy);
-        const double a1 = M.line_aul[n1], b1 = M.line_alu[n1], a2 = M.line_aul[n2], b2 = M.line_alu[n2];
-        const double em1 = c * a1 * pop[u1];
-        double op1 = c * (b1 * pop[l1] - a1 * pop[u1]) + MIN_LINE_OPACITY;
-        const double em2 = c * a2 * pop[u2];
-        double op2 = c * (b2 * pop[l2] - a2 * pop[u2]) + MIN_LINE_OPACITY;
-        if (op1 < 0.) op1 *= INV_TRANS_FACTOR;
-        if (op2 < 0.) op2 *= INV_TRANS_FACTOR;
-        const double g1 = fabs(sm.vgrad) / (sm.vw * op1), g2 = fabs(sm.vgrad) / (sm.vw * op2);
-        const double delta = fabs(sm.vgrad) / (sm.vw * dust_opacity(P, M, sm, n1));
-        double dx = (P.energy[u1] - P.energy[l1] - P.energy[u2] + P.energy[l2]) * SPEED_OF_LIGHT / (energy * sm.vw);
-        if (sm.vgrad < 0.) dx *= -1.;
-        const bool near = fabs(dx) < max_dx, far = fabs(dx) > max_dx - 0.5;
-        double ep1 = 0., ep2 = 0., ep01 = 0., ep02 = 0., q1 = 0., q2 = 0.;
-        if (near) {
-            const double ld = lvg_log10(delta);
-            const OvIdx A = ov_index(P, G, g1, ld, g2 / g1, dx), B = ov_index(P, G, g2, ld, g1 / g2, -dx);
-            double v1[16], v2[16], w1[16], w2[16];
-            ov_load(P, P.ov_p1, A, v1);
-            ov_load(P, P.ov_p1, B, v2);
-            ov_load(P, P.ov_p2, A, w1);
-            ov_load(P, P.ov_p2, B, w2);
-            ep1 = ov_sum(A, v1);
-            ep2 = ov_sum(B, v2);
-            q1 = ov_sum(A, w1);
-            q2 = ov_sum(B, w2);
-        }
-        if (far) {
-            const EscIdx A = esc_index(P, G, g1, delta), B = esc_index(P, G, g2, delta);
-            double v1[4], v2[4];
-            esc_load(P, A, v1);
-            esc_load(P, B, v2);
-            ep01 = esc_sum(A, v1);
-            ep02 = esc_sum(B, v2);
-        }
-        if (fabs(dx) > max_dx) { ep1 = ep01; ep2 = ep02; }
-        else if (far) {
-            c = 2. * (max_dx - fabs(dx));
-            ep1 = ep01 * (1. - c) + ep1 * c;
-            ep2 = ep02 * (1. - c) + ep2 * c;
-        }
-        double i1 = em1 / op1 * ep1;
-        double i2 = em2 / op2 * ep2;
-        if (near) {
-            ep1 = q1;
-            ep2 = q2;
-            if (far) {
-                c = 2. * (max_dx - fabs(dx));
-                ep1 *= c; ep2 *= c;
-            }
-            i1 += em2 / op2 * ep1;
-            i2 += em1 / op1 * ep2;
-        }
-        sm.y[2 * n1] = a1 * (1. + i1);
-        sm.y[2 * n1 + 1] = b1 * i1;
-        sm.y[2 * n2] = a2 * (1. + i2);
-        sm.y[2 * n2 + 1] = b2 * i2;
-    }
-}
-
 // LU with partial pivoting of the register rows a (lane = physical row) and the
 // right-hand side rb, then back substitution; x[k] (LDS) receives solution k.
 // Same operation sequence as oracle_lu_solve: pivot = first maximum |a_ik| in the
 // oracle's (physically swapped) row order, tracked here as each row's logical
 // position lp; every a_ij receives fma(-l_ik, u_kj, a_ij) for k ascending; x_k =
 // b_k / u_kk and b_i = fma(-u_ik, x_k, b_i) for k descending.
-#ifndef LVG_WAVE_LOOKAHEAD
-#define LVG_WAVE_LOOKAHEAD 1          // next column's pivot reduction overlapped with this column's update
-#endif
-#ifndef LVG_WAVE_LDS_BCAST
-#define LVG_WAVE_LDS_BCAST 0          // 1: pivot row broadcast through LDS (measured slower than v_readlane)
-#endif
+// Look-ahead pivot search: column c+1 is updated first and its max-key reduction (a
+// dependent DPP chain) is issued before the rest of column c's row update, so the two
+// overlap.
 template <int NM>
-__device__ __forceinline__ void wave_lu_solve(double (&a)[NM], double rb, int N, double *x, double *pb) {
+__device__ __forceinline__ void wave_lu_solve(double (&a)[NM], double rb, int N, double *x) {
     const int ln = lane_id();
     TSTAMP(tf0);
     bool act = ln < N;
     int lp = ln;
-#if LVG_WAVE_LOOKAHEAD
-    // Look-ahead pivot search: column c+1 is updated first and its max-key reduction (a
-    // dependent DPP chain) is issued before the rest of column c's row update, so the two
-    // overlap. Same pivots and the same fma per element as the plain loop below.
     unsigned khi, klo, H;
-    auto col_key = [&](int c, double v) {
-        const double av = fabs(v);
-        const unsigned long long bits = (act && av == av) ? (unsigned long long)__double_as_longlong(av) : 0ull;
-        const bool dnan = act && lp == c && av != av;
-        khi = dnan ? 0xffffffffu : act ? ((unsigned)(bits >> 32) | 0x80000000u) : 0u;
-        klo = dnan ? 0xffffffffu : (unsigned)bits;
-    };
-    col_key(0, a[0]);
+    pivot_key(a[0], act, lp == 0, khi, klo);
     H = wave_max_u32(khi);
 #pragma unroll
     for (int c = 0; c < NM; c++) {
@@ -607,7 +431,7 @@ __device__ __forceinline__ void wave_lu_solve(double (&a)[NM], double rb, int N,
             if (c + 1 < NM) {
                 const double u = readlane_d(a[c + 1], pl);
                 a[c + 1] = act ? fma(-l, u, a[c + 1]) : a[c + 1];
-                col_key(c + 1, a[c + 1]);
+                pivot_key(a[c + 1], act, lp == c + 1, khi, klo);
                 H = wave_max_u32(khi);
             }
 #pragma unroll
@@ -618,76 +442,6 @@ __device__ __forceinline__ void wave_lu_solve(double (&a)[NM], double rb, int N,
             if (act) { a[c] = l; rb = fma(-l, bc, rb); }
         }
     }
-#else
-#pragma unroll
-    for (int c = 0; c < NM; c++) {
-        if (c < N) {
-            const double av = fabs(a[c]);
-            const unsigned long long bits = (act && av == av) ? (unsigned long long)__double_as_longlong(av) : 0ull;
-            // oracle_lu_solve: amax seeded with |a_kk|, replaced on a strict '>' -> a NaN below
-            // never wins, a NaN on the diagonal (logical position c) always does
-            const bool dnan = act && lp == c && av != av;
-            const unsigned hi = dnan ? 0xffffffffu : act ? ((unsigned)(bits >> 32) | 0x80000000u) : 0u;
-            const unsigned lo = dnan ? 0xffffffffu : (unsigned)bits;
-            const unsigned H = wave_max_u32(hi);
-            const unsigned long long tie = __ballot(hi == H);
-            int pl;
-            if (__popcll(tie) == 1) {
-                pl = __ffsll((long long)tie) - 1;
-            } else {
-                const unsigned Lw = wave_max_u32(hi == H ? lo : 0u);
-                const unsigned X = wave_max_u32((hi == H && lo == Lw && act) ? ~(unsigned)lp : 0u);
-                const int wmin = (int)~X;
-                pl = __ffsll((long long)__ballot(act && hi == H && lo == Lw && lp == wmin)) - 1;
-            }
-            pl = __builtin_amdgcn_readfirstlane(pl);
-            const int plp = __builtin_amdgcn_readlane(lp, pl);
-            double piv, bc;
-            if (LVG_WAVE_LDS_BCAST) {
-                // the pivot lane stores its row from column c (16-byte pairs from c & ~1) and
-                // its b; every lane reads them back (LDS is in order within a wave)
-                const int c2 = c & ~1;
-                if (ln == pl) {
-#pragma unroll
-                    for (int j = c2; j < NM; j += 2)
-                        *reinterpret_cast<double2 *>(pb + j) = make_double2(a[j], j + 1 < NM ? a[j + 1] : 0.);
-                    pb[NM + (NM & 1)] = rb;
-                }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                double u[NM];
-#pragma unroll
-                for (int j = c2; j < NM; j += 2) {
-                    const double2 v = *reinterpret_cast<const double2 *>(pb + j);
-                    u[j] = v.x;
-                    if (j + 1 < NM) u[j + 1] = v.y;
-                }
-                piv = u[c];
-                bc = pb[NM + (NM & 1)];
-                if (ln == pl) { act = false; lp = c; }
-                else if (lp == c) lp = plp;
-                const double l = a[c] / piv;
-#pragma unroll
-                for (int j = c + 1; j < NM; j++)
-                    if (act) a[j] = fma(-l, u[j], a[j]);
-                if (act) { a[c] = l; rb = fma(-l, bc, rb); }
-                __builtin_amdgcn_wave_barrier();    // reads of pb done before the next column's stores
-            } else {
-                piv = readlane_d(a[c], pl);
-                bc = readlane_d(rb, pl);
-                if (ln == pl) { act = false; lp = c; }
-                else if (lp == c) lp = plp;
-                const double l = a[c] / piv;
-#pragma unroll
-                for (int j = c + 1; j < NM; j++) {
-                    const double u = readlane_d(a[j], pl);
-                    if (act) a[j] = fma(-l, u, a[j]);
-                }
-                if (act) { a[c] = l; rb = fma(-l, bc, rb); }
-            }
-        }
-    }
-#endif
     TACC(PH_PANEL, tf0);
     TSTAMP(tb0);
 #pragma unroll
@@ -732,18 +486,16 @@ __device__ __forceinline__ void wave_accel_step(Ctl &C, Slot &S, int N, WaveLaye
         int i, j;
         if (t < np * np) { i = t / np; j = t - i * np; } else { i = t - np * np; j = -1; }
         const double *ri = ring(S.res, C.hr, i + 1, N);
-        const double *rj = (j >= 0) ? ring(S.res, C.hr, j + 1, N) : nullptr;
+        const double *rj = (j >= 0) ? ring(S.res, C.hr, j + 1, N) : ri;
         double a = 0.;
-#if LVG_WAVE_ACCEL_BATCH
         // the ring reads of 8 levels issued together (one round trip per block), the sum
         // still taken for k ascending
-        const double *rjj = (j >= 0) ? rj : ri;
         for (int k0 = 0; k0 < N; k0 += 8) {
             double pv[8], r0v[8], riv[8], rjv[8];
 #pragma unroll
             for (int u = 0; u < 8; u++) {
                 const int k = (k0 + u < N) ? k0 + u : k0;
-                pv[u] = p0[k]; r0v[u] = r0[k]; riv[u] = ri[k]; rjv[u] = rjj[k];
+                pv[u] = p0[k]; r0v[u] = r0[k]; riv[u] = ri[k]; rjv[u] = rj[k];
             }
 #pragma unroll
             for (int u = 0; u < 8; u++) {
@@ -754,61 +506,20 @@ __device__ __forceinline__ void wave_accel_step(Ctl &C, Slot &S, int N, WaveLaye
                 }
             }
         }
-#else
-        for (int k = 0; k < N; k++) {
-            double w = p0[k] + 1.e-99;
-            double num = (j >= 0) ? (r0[k] - ri[k]) * (r0[k] - rj[k]) : (r0[k] - ri[k]) * r0[k];
-            a = a + num / (w * w);
-        }
-#endif
         sm.hist_acc[t] = a;
     }
     wave_sync();
-    if (t == 0) {
-        double Am[4][4], bv[4];
-        for (int i = 0; i < np; i++) {
-            for (int j = 0; j < np; j++) Am[i][j] = sm.hist_acc[i * np + j];
-            bv[i] = sm.hist_acc[np * np + i];
-        }
-        for (int k = 0; k < np; k++) {
-            int p = k;
-            double amax = fabs(Am[k][k]);
-            for (int i = k + 1; i < np; i++) if (fabs(Am[i][k]) > amax) { amax = fabs(Am[i][k]); p = i; }
-            if (p != k) {
-                for (int j = 0; j < np; j++) { double x = Am[k][j]; Am[k][j] = Am[p][j]; Am[p][j] = x; }
-                double x = bv[k]; bv[k] = bv[p]; bv[p] = x;
-            }
-            double piv = Am[k][k];
-            for (int i = k + 1; i < np; i++) {
-                double l = Am[i][k] / piv;
-                Am[i][k] = l;
-                for (int j = k + 1; j < np; j++) Am[i][j] = fma(-l, Am[k][j], Am[i][j]);
-                bv[i] = fma(-l, bv[k], bv[i]);
-            }
-        }
-        for (int k = np - 1; k >= 0; k--) {
-            bv[k] /= Am[k][k];
-            double x = bv[k];
-            for (int i = 0; i < k; i++) bv[i] = fma(-Am[i][k], x, bv[i]);
-        }
-        double sum = 0.;
-        for (int i = 0; i < np; i++) { sum = sum + bv[i]; sm.hist_acc[16 + i] = bv[i]; }
-        sm.hist_acc[31] = sum;
-    }
+    if (t == 0) accel_solve_small(sm.hist_acc, np);
     wave_sync();
     const double sum = sm.hist_acc[31];
     for (int k = t; k < N; k += 64) {
         double a = (1. - sum) * p0[k];
-#if LVG_WAVE_ACCEL_BATCH
         double pv[4];                   // np <= 4 (accel_nb <= 5, checked by the host)
 #pragma unroll
         for (int i = 0; i < 4; i++) pv[i] = (i < np) ? ring(S.prev, C.hp, i + 1, N)[k] : 0.;
 #pragma unroll
         for (int i = 0; i < 4; i++)
             if (i < np) a = a + sm.hist_acc[16 + i] * pv[i];
-#else
-        for (int i = 0; i < np; i++) a = a + sm.hist_acc[16 + i] * ring(S.prev, C.hp, i + 1, N)[k];
-#endif
         sm.pold[k] = a;
     }
     wave_sync();
@@ -890,9 +601,8 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
     // line invariants after the y region of the slot (host: ensure_workspace)
     const int inv_cap = P.plain.nb_lines > P.overlap.nb_lines ? P.plain.nb_lines : P.overlap.nb_lines;
     double *inv = S.y + 2 * inv_cap + 64;
-    if (LVG_WAVE_LINE_INV) wave_line_invariants(P, G, M, sm, Lc.line_overlap != 0, inv, inv_cap);
-    if (LVG_WAVE_LINE_INV || (need_boundary && !from_prev)) wave_sync_global();   // B is read across lanes
-    else wave_sync();
+    wave_line_invariants(P, G, M, sm, Lc.line_overlap != 0, inv, inv_cap);
+    wave_sync_global();             // B and the invariants are read across lanes
     TACC(PH_SETUP, ts0);
     if (!need_boundary) {
         if (t < N) { sm.pold[t] = pops[t]; S.given[t] = pops[t]; }
@@ -907,7 +617,6 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
     bool boundary = need_boundary && !from_prev, found = false;
     int iters = 0, retry = 0;
     const int row = t < N ? t : 0;
-#if LVG_WAVE_KROW
     // the lane's row of K and of the line-index map, fixed for the layer, in registers
     double krow[NM];
     int lrow[NM];
@@ -917,16 +626,16 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
         krow[j] = K[row * ldk + jj];
         lrow[j] = (j < N) ? li[row * ldk + jj] : -1;
     }
-#endif
     if (!boundary) wave_start_pass(C, S, Lc, N, accel ? Lc.max_iter_acc : Lc.max_iter_plain, accel);
     for (;;) {
         double a[NM];
         double eq = 0.;
         // N through an opaque SGPR copy each pass: otherwise the compiler hoists every
         // N-derived lane mask and K address of the unrolled loops out of the layer loop and
-        // spills them (v_writelane / v_readlane + s_nop on every use)
+        // spills them (v_writelane / v_readlane + s_nop on every use); measured: helps
+        // NM = 24, hurts NM = 48
         int N = P.N;
-        if (LVG_WAVE_OPAQUE_N && NM <= 32) asm volatile("" : "+s"(N));   // measured: helps NM=24, hurts NM=48
+        if (NM <= 32) asm volatile("" : "+s"(N));
         if (boundary) {
             TSTAMP(tbd);
             wave_boundary_rows<NM>(S.A, N, a);
@@ -937,17 +646,15 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
             TACC(PH_CTL, tc0);
             TSTAMP(tl0);
             // line terms y (compute_line_terms)
-            if (LVG_WAVE_LINE_INV) {
-                if (Lc.line_overlap) wave_line_terms_overlap_inv(P, G, M, sm, inv, inv_cap);
-                else wave_line_terms_plain_inv(P, G, M, sm, inv, inv_cap);
-            } else if (Lc.line_overlap) wave_line_terms_overlap(P, G, M, sm);
-            else wave_line_terms_plain(P, G, M, sm);
+            if (Lc.line_overlap) wave_line_terms_overlap(P, G, M, sm, inv, inv_cap);
+            else wave_line_terms_plain(P, G, M, sm, inv, inv_cap);
             wave_sync();
             TACC(PH_LINES, tl0);
             TSTAMP(ta0);
             // diagonal (column_diagonals): lane d folds column d of K in the reference order.
-            // Operands come in blocks of 8 (all LDS loads of a block issued before use) and
-            // the data-dependent terms are selects, not branches: same operations, same order.
+            // Operands come in blocks of 8 (all LDS loads of a block issued before use, row 0
+            // standing in past N) and the data-dependent terms are selects, not branches:
+            // same operations, same order.
             double dg = 0.;
             {
                 const int d = row;
@@ -959,15 +666,10 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
 #pragma unroll
                     for (int u = 0; u < 8; u++) {
                         const int r = r0 + u;
-                        if (LVG_WAVE_CLAMP) {   // unconditional LDS reads (row 0 stands in past N)
-                            const int rr = (r < N) ? r : 0;
-                            kc[u] = K[rr * ldk + d];
-                            const int lv = li[rr * ldk + d];
-                            lc[u] = (il && r < N) ? lv : -1;
-                        } else {
-                            kc[u] = (r < N) ? K[r * ldk + d] : 0.;
-                            lc[u] = (il && r < N) ? li[r * ldk + d] : -1;
-                        }
+                        const int rr = (r < N) ? r : 0;
+                        kc[u] = K[rr * ldk + d];
+                        const int lv = li[rr * ldk + d];
+                        lc[u] = (il && r < N) ? lv : -1;
                     }
 #pragma unroll
                     for (int u = 0; u < 8; u++) yc[u] = sm.y[lc[u] >= 0 ? lc[u] : 0];
@@ -993,23 +695,9 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
                     const int j = j0 + u;
-                    if (LVG_WAVE_KROW) {
-#if LVG_WAVE_KROW
-                        kc[u] = krow[j];
-                        lc[u] = lrow[j];
-                        pc[u] = sm.pold[j];
-#endif
-                    } else if (LVG_WAVE_CLAMP) {
-                        const int jj = (j < N) ? j : 0;
-                        kc[u] = K[row * ldk + jj];
-                        const int lv = li[row * ldk + jj];
-                        lc[u] = (j < N) ? lv : -1;
-                        pc[u] = sm.pold[j];        // j < NM <= WNMAX
-                    } else {
-                        kc[u] = (j < N) ? K[row * ldk + j] : 0.;
-                        lc[u] = (j < N) ? li[row * ldk + j] : -1;
-                        pc[u] = (j < N) ? sm.pold[j] : 0.;
-                    }
+                    kc[u] = krow[j];
+                    lc[u] = lrow[j];
+                    pc[u] = sm.pold[j];        // j < NM <= WNMAX
                 }
 #pragma unroll
                 for (int u = 0; u < 8; u++) yc[u] = sm.y[lc[u] >= 0 ? lc[u] : 0];
@@ -1031,7 +719,7 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
             eq = wave_max(t < N ? fabs(s) : 0.);
             TACC(PH_ASSEMBLE, ta0);
         }
-        wave_lu_solve<NM>(a, t == 0 ? 1. : 0., N, sm.pnew, sm.prow);
+        wave_lu_solve<NM>(a, t == 0 ? 1. : 0., N, sm.pnew);
         wave_sync();
         if (boundary) {
             if (t < N) { sm.pold[t] = sm.pnew[t]; S.given[t] = sm.pnew[t]; }
@@ -1074,8 +762,8 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
 }
 
 template <int NM>
-__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) solve_wave_kernel(const LvgDevProblem *__restrict__ Pp,
-                                                            const LvgLaunch *__restrict__ Lp) {
+__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
+solve_wave_kernel(const LvgDevProblem *__restrict__ Pp, const LvgLaunch *__restrict__ Lp) {
     __shared__ WaveShared sh;
     const LvgDevProblem &P = *Pp;
     const LvgLaunch &Lc = *Lp;
@@ -1135,9 +823,60 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
     PH_FLUSH();
 }
 
-// host-side plan: waves per block and dynamic LDS bytes for N, or 0 if the wave
-// kernel does not apply (N > 64, too many line terms or grid points for LDS)
+// host-side plan: dynamic LDS bytes of wpb waves for N levels
 inline size_t wave_dyn_bytes(int N, int wpb) {
     const int ldk = N | 1;
     return sizeof(double) * ((size_t)(N * ldk + 1) / 2 + (size_t)wpb * N * ldk);
 }
+
+}  // namespace lvg
+
+// 1 and the waves per block / dynamic LDS bytes if the wave kernel applies to N levels
+// with nb_y line terms and grid_doubles escape-grid points; 0 if not.
+extern "C" int lvg_wave_plan(int N, int nb_y, int grid_doubles, size_t lds_cap, int *wpb, size_t *dyn) {
+    if (N < 2 || N > lvg::WNMAX || nb_y > lvg::WYCAP || grid_doubles > lvg::WGRID_CAP) return 0;
+    for (int w = 4; w >= 1; w >>= 1) {
+        const size_t d = lvg::wave_dyn_bytes(N, w);
+        if (sizeof(lvg::WaveShared) + d <= lds_cap) { *wpb = w; *dyn = d; return 1; }
+    }
+    return 0;
+}
+
+// instantiations every 8 levels from 24 up (the unrolled row loops run to NM): OH-HF 24
+// and p-H2O 45 run NM = 24 and 48, the reference's OH-HF 56 runs NM = 56
+#define LVG_WAVE_NMS(X) X(16) X(24) X(32) X(40) X(48) X(56) X(64)
+static int wave_nm(int N) { return N <= 16 ? 16 : ((N + 7) / 8) * 8; }
+static const void *wave_kernel(int N) {
+#define LVG_WK(NM_) if (wave_nm(N) == NM_) return reinterpret_cast<const void *>(&lvg::solve_wave_kernel<NM_>);
+    LVG_WAVE_NMS(LVG_WK)
+#undef LVG_WK
+    return nullptr;
+}
+
+extern "C" hipError_t lvg_wave_occupancy(int N, int wpb, size_t dyn, int *blocks_per_cu) {
+    const void *k = wave_kernel(N);
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+    if (e != hipSuccess) return e;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 64 * wpb, dyn);
+}
+
+extern "C" hipError_t lvg_launch_solve_wave(const LvgDevProblem *P, const LvgLaunch *L, int N, int grid, int wpb,
+                                            size_t dyn, hipStream_t s) {
+    const dim3 g(grid), b(64 * wpb);
+#define LVG_WL(NM_) if (wave_nm(N) == NM_) hipLaunchKernelGGL(lvg::solve_wave_kernel<NM_>, g, b, dyn, s, P, L);
+    LVG_WAVE_NMS(LVG_WL)
+#undef LVG_WL
+    return hipGetLastError();
+}
+extern "C" size_t lvg_wave_static_lds(void) { return sizeof(lvg::WaveShared); }
+
+#ifdef LVG_PHASE_TIMERS
+extern "C" int lvg_debug_wave_phase_cycles(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lvg::lvg_phase_cycles), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[32] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(lvg::lvg_phase_cycles), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

@@ -21,7 +21,7 @@ EXPORTS = ("lvg_abi_version", "lvg_solve_opts_default", "lvg_create", "lvg_destr
            "lvg_nb_lev", "lvg_solve_layers", "lvg_layer_soa_rows", "lvg_solve_layers_device",
            "lvg_debug_calc_new_pop", "lvg_boundary_layer_populations", "lvg_find_opts_default",
            "lvg_find_transitions", "lvg_lim_luminosity", "lvg_last_kernel_time", "lvg_solve_chains",
-           "lvg_solve_chains_device", "lvg_last_coll_time")
+           "lvg_solve_chains_device", "lvg_last_coll_time", "lvg_set_tuning")
 
 _lib = None
 
@@ -55,6 +55,7 @@ def load(path: str = LIB_PATH):
     L.lvg_boundary_layer_populations.argtypes = [vp, vp, dp]
     L.lvg_last_kernel_time.argtypes = [vp, dp, C.POINTER(C.c_int)]
     L.lvg_last_coll_time.argtypes = [vp, dp]
+    L.lvg_set_tuning.argtypes = [vp, C.c_char_p]
     L.lvg_find_opts_default.argtypes = [vp]
     ip = C.POINTER(C.c_int)
     L.lvg_lim_luminosity.argtypes = [vp, vp, vp, dp, i, ip, ip, i, dp, dp, dp, dp, dp, dp]
@@ -147,6 +148,10 @@ class LvgSolver:
         n = C.c_int()
         self._check(self.lib.lvg_last_kernel_time(self.h, C.byref(ms), C.byref(n)), "lvg_last_kernel_time")
         return ms.value, n.value
+
+    def set_tuning(self, spec: str = ""):
+        """lvg_set_tuning: "key=value,..." (include/lvg_amd.h); never changes a result."""
+        self._check(self.lib.lvg_set_tuning(self.h, spec.encode()), "lvg_set_tuning")
 
     def last_coll_time(self):
         """Milliseconds of the collision-operator kernel of the last solve (0: not run)."""

@@ -1,7 +1,4 @@
 """Shared checks of the GPU parity tests (test infrastructure)."""
-import contextlib
-import os
-
 import numpy as np
 
 
@@ -15,26 +12,6 @@ def assert_same(pg, sg, po, so, equal_nan=False):
     same = (pg == po) | (np.isnan(pg) & np.isnan(po)) if equal_nan else (pg == po)
     bad = np.argwhere(~same)
     assert bad.size == 0, f"{len(bad)} population entries differ, first {bad[:3].tolist()}"
-
-
-@contextlib.contextmanager
-def env(**kv):
-    """Set (value) or unset (None) environment variables for the duration (read by the
-    library through getenv at each solve: LVG_BLOCK_KERNEL, LVG_INDEX_ORDER, ...)."""
-    old = {k: os.environ.get(k) for k in kv}
-    try:
-        for k, v in kv.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-        yield
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
 
 
 def overlap_dx(prob, layers):

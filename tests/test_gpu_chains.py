@@ -14,7 +14,7 @@ import pytest
 from radiative_transfer_amd import abi, synth
 from radiative_transfer_amd.native import LvgError, LvgSolver
 from oracle import oracle
-from parity_helpers import assert_same, env
+from parity_helpers import assert_same
 
 pytestmark = pytest.mark.gpu
 
@@ -37,13 +37,13 @@ def test_chains_bit_exact(name, nl, force_block):
     cuts = sorted({0, nl, 1, nl // 3, nl // 3, (2 * nl) // 3})
     off = np.array(cuts + ([nl] if cuts[-1] != nl else []), dtype=np.int32)
     off = np.concatenate([off[:2], off[1:2], off[2:]])            # duplicate offset: empty chain
-    with env(LVG_BLOCK_KERNEL="1" if force_block else None):
-        po, so = _cmp_chains(s, P, L, off, abi.default_opts(init=WARM, **o))
-        # caps that leave layers unconverged mid-chain: the next layer restarts from the
-        # boundary populations (the is_solution_found_prev branch)
-        kw = {"max_iter_acc": 3, "allow_plain_retry": 0} if o.get("acceleration", 1) else {"max_iter_plain": 3}
-        po, so = _cmp_chains(s, P, L, off, abi.default_opts(init=WARM, **{**o, **kw}))
-        assert (so["converged"] == 0).any() and (so["converged"] == 1).any()
+    s.set_tuning("block_kernel=1" if force_block else "")
+    po, so = _cmp_chains(s, P, L, off, abi.default_opts(init=WARM, **o))
+    # caps that leave layers unconverged mid-chain: the next layer restarts from the
+    # boundary populations (the is_solution_found_prev branch)
+    kw = {"max_iter_acc": 3, "allow_plain_retry": 0} if o.get("acceleration", 1) else {"max_iter_plain": 3}
+    po, so = _cmp_chains(s, P, L, off, abi.default_opts(init=WARM, **{**o, **kw}))
+    assert (so["converged"] == 0).any() and (so["converged"] == 1).any()
     s.close()
 
 

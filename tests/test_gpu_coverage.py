@@ -23,7 +23,7 @@ import pytest
 from radiative_transfer_amd import abi, synth
 from radiative_transfer_amd.native import LvgSolver
 from oracle import oracle
-from parity_helpers import assert_same, env, overlap_dx
+from parity_helpers import assert_same, overlap_dx
 
 pytestmark = pytest.mark.gpu
 
@@ -39,25 +39,25 @@ def _cmp(s, P, L, opts, pops=None, equal_nan=False):
 def test_block_kernel_option_paths(name, nl, force_block):
     P, L, o = synth.make_problem(name, nb_lay=nl)
     s = LvgSolver(P)
-    with env(LVG_BLOCK_KERNEL="1" if force_block else None):
-        variants = [{"accel_start": 2, "accel_nb": 2, "accel_period": 1},                 # Ng from iteration 2
-                    {"accel_start": 3, "accel_nb": 3, "accel_period": 2, "max_iter_acc": 9},
-                    {"max_iter_acc": 2, "allow_plain_retry": 0},                          # cap -> best iterate
-                    {"max_iter_acc": 2, "allow_plain_retry": 1, "max_iter_plain": 3},      # forced plain retry
-                    {"acceleration": 0, "max_iter_plain": 2}]
-        ran_accel = False
-        for kw in variants:
-            opts = abi.default_opts(**{**o, **kw})
-            po, so = _cmp(s, P, L, opts)
-            if opts.acceleration and (so["iterations"] > opts.accel_start).any():
-                ran_accel = True
-        assert ran_accel, "no layer reached the Ng step"
-        # init modes
-        base = abi.default_opts(**o)
-        p0, _ = oracle.solve_layers(P, L, base)
-        guess = 0.5 * p0 + 0.5 / P.mol.nb_lev
-        _cmp(s, P, L, abi.default_opts(init=abi.LVG_INIT_GIVEN, **o), pops=guess)
-        _cmp(s, P, L, abi.default_opts(init=abi.LVG_INIT_WARM_CHAIN, **o))
+    s.set_tuning("block_kernel=1" if force_block else "")
+    variants = [{"accel_start": 2, "accel_nb": 2, "accel_period": 1},                 # Ng from iteration 2
+                {"accel_start": 3, "accel_nb": 3, "accel_period": 2, "max_iter_acc": 9},
+                {"max_iter_acc": 2, "allow_plain_retry": 0},                          # cap -> best iterate
+                {"max_iter_acc": 2, "allow_plain_retry": 1, "max_iter_plain": 3},      # forced plain retry
+                {"acceleration": 0, "max_iter_plain": 2}]
+    ran_accel = False
+    for kw in variants:
+        opts = abi.default_opts(**{**o, **kw})
+        po, so = _cmp(s, P, L, opts)
+        if opts.acceleration and (so["iterations"] > opts.accel_start).any():
+            ran_accel = True
+    assert ran_accel, "no layer reached the Ng step"
+    # init modes
+    base = abi.default_opts(**o)
+    p0, _ = oracle.solve_layers(P, L, base)
+    guess = 0.5 * p0 + 0.5 / P.mol.nb_lev
+    _cmp(s, P, L, abi.default_opts(init=abi.LVG_INIT_GIVEN, **o), pops=guess)
+    _cmp(s, P, L, abi.default_opts(init=abi.LVG_INIT_WARM_CHAIN, **o))
     s.close()
 
 
@@ -112,12 +112,12 @@ def _generic_problem():
 def test_collision_rules(make, force_block):
     P, L, o = make()
     s = LvgSolver(P)
-    with env(LVG_BLOCK_KERNEL="1" if force_block else None):
-        _cmp(s, P, L, abi.default_opts(**o))
-        bo = oracle.boundary_layer_populations(P, L)
-        Mg, dfg, pg, eg = s.debug_calc_new_pop(L, 0, bo[0], 0)
-        Mo, dfo, po, eo = oracle.calc_new_pop(P, L, 0, bo[0], 0)
-        assert np.array_equal(Mg, Mo) and np.array_equal(pg, po)
+    s.set_tuning("block_kernel=1" if force_block else "")
+    _cmp(s, P, L, abi.default_opts(**o))
+    bo = oracle.boundary_layer_populations(P, L)
+    Mg, dfg, pg, eg = s.debug_calc_new_pop(L, 0, bo[0], 0)
+    Mo, dfo, po, eo = oracle.calc_new_pop(P, L, 0, bo[0], 0)
+    assert np.array_equal(Mg, Mo) and np.array_equal(pg, po)
     # the rule matters: the rates differ from a 3-table OH-HF / base reading of the same tables
     for lay in (0, 5):
         d, u, de, ue = oracle.coll_rates(P, L, lay)
@@ -179,4 +179,28 @@ def test_async_device_solve_then_host_entry_on_same_handle():
     pob, sob = oracle.solve_layers(P, B, opts)
     assert_same(pa, sa, poa, soa_)
     assert_same(pb, sb, pob, sob)
+    s.close()
+
+
+@pytest.mark.parametrize("make", [lambda: synth.make_problem("ch3oha256_4096", nb_lay=12), _generic_problem],
+                         ids=["ch3oha256", "generic_electrons"])
+def test_collision_build_paths(make):
+    """Independent layers on the block kernel with the collision operators built in the
+    solve kernel (the default), built ahead by coll_kernel (B formed from K without
+    electron tables, B stored with them), and with coll_kernel asked for but over its
+    memory budget (the fallback to the in-kernel build): all bit-exact against the
+    oracle (coll_rates.cpp:152-174 per layer, iteration_lvg.cpp:118-131)."""
+    P, L, o = make()
+    s = LvgSolver(P)
+    opts = abi.default_opts(**o)
+    po, so = oracle.solve_layers(P, L, opts)
+    for spec, ahead in (("block_kernel=1", False), ("block_kernel=1,coll_ahead=1", True),
+                        ("block_kernel=1,coll_ahead=1,coll_order=0", True),
+                        ("block_kernel=1,coll_ahead=1,coll_mem=0", False)):
+        s.set_tuning(spec)
+        pg, sg = s.solve_layers(L, opts)
+        assert_same(pg, sg, po, so)
+        assert (s.last_coll_time() > 0) == ahead, spec
+    with pytest.raises(Exception):
+        s.set_tuning("no_such_key=1")
     s.close()
