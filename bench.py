@@ -144,8 +144,8 @@ def _smi_finish(p) -> dict:
         pick = {}
         for k, v in d.items():
             kl = k.lower()
-            if ("sclk" in kl or "mclk" in kl) and "clock level" in kl:
-                pick[k.split("(")[0].strip()] = v
+            if "sclk" in kl or "mclk" in kl or "fclk" in kl:
+                pick[k.strip().rstrip(":")] = v
             elif "power" in kl and "(w)" in kl:
                 pick["power_w"] = v
             elif "unique id" in kl or "serial" in kl or kl.startswith("card series") or kl.startswith("card sku"):
