@@ -46,9 +46,24 @@ namespace LVG_NS {
 
 #include "lvg_common.h"
 
+#if defined(LVG_PHASE_TIMERS) && !LVG_BIG
+// timer build of the 256-thread kernel: lane 0 of every wave accumulates (LDS atomics), so
+// the phases of waves that work while wave 0 waits are counted too (sums over 4 waves)
+#undef TACC
+#define TACC(ph, v0) do { if ((threadIdx.x & 63) == 0) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    atomicAdd(&lvg_ph_lds[ph], t_ - (v0)); } } while (0)
+#endif
+
 constexpr int BT   = LVG_BIG ? 768 : 256;   // threads per workgroup (one panel row per thread: N <= BT)
 constexpr int NMAX = BT;                    // max levels of this kernel
-constexpr int OCC  = LVG_BIG ? 1 : 2;       // resident workgroups per CU the kernel is built for
+#ifndef LVG_OCC
+#define LVG_OCC (LVG_BIG ? 1 : 2)
+#endif
+#ifndef LVG_LU_CW
+#define LVG_LU_CW 16
+#endif
+constexpr int OCC  = LVG_OCC;               // resident workgroups per CU the kernel is built for
+constexpr int LU_CW = LVG_LU_CW;            // N <= 256 LU: columns per wave (lvg_lu256.h)
 constexpr int NW   = BT / 64;
 constexpr int NB   = 16;                    // LU panel width (chunk)
 static_assert(NMAX <= BT && BT % 64 == 0 && NMAX % 32 == 0, "one row per thread, whole waves");
@@ -57,15 +72,15 @@ constexpr int TC = 4;                       // columns per thread in the LU regi
 constexpr int TR = NMAX * 8 / BT;           // tile rows per thread: the BT/8 row groups cover NMAX
 static_assert(TR * (BT / 8) >= NMAX && TR % 2 == 0, "the register tiles cover every row");
 constexpr int WB = 8 * TC;                  // LU block-column width
-constexpr int COLL_PU = 4;                  // 16x16 pair tiles per batch of the in-kernel collision build
+#ifndef LVG_COLL_PU
+#define LVG_COLL_PU 4
+#endif
+constexpr int COLL_PU = LVG_COLL_PU;        // 16x16 pair tiles per batch of the in-kernel collision build
 
+#if LVG_BIG
 struct Smem {
     double pold[NMAX], bvec[NMAX];
-#if LVG_BIG
     union { double pnew[NMAX]; double blog[NMAX]; };   // pnew only ever copies blog
-#else
-    double pnew[NMAX], blog[NMAX];
-#endif
     double diag[NMAX];          // assembled diagonal of the rate matrix (fused assembly)
     double ylds[YCAP];          // line terms y of the current iteration (if they fit)
     int    tmap[NMAX];          // physical row of each tile row at the current block load
@@ -75,7 +90,6 @@ struct Smem {
     int    ired[2 * NW];
     unsigned long long pkey[2 * NW];   // panel: per-wave pivot keys (|v| bits, active flag), double buffered
     alignas(16) double cand[2][NW][NB + 2]; // panel: each wave's pivot candidate row and its b, double buffered
-    int    candp[2][NW];        // its physical row
     double L11[NB][NB + 1];
     alignas(16) double Ub[2][NB][WB + 2];   // U rows of one chunk across the block column (by chunk parity)
     union alignas(16) {
@@ -83,6 +97,25 @@ struct Smem {
         double LT[NB][NMAX];    // L of one chunk, transposed, physical rows
         double hist_acc[32];    // accel_step sums (used outside the LU only)
     } pu;
+#else
+struct Smem {
+    double pold[NMAX], bvec[NMAX];
+    union { double pnew[NMAX]; double blog[NMAX]; };   // pnew only ever copies blog
+    double diag[NMAX];          // assembled diagonal of the rate matrix (fused assembly)
+    double resid[NMAX];         // residual rows (physical), handed from wave to wave in column order
+    double ylds[YCAP];          // line terms y of the current iteration (if they fit)
+    int    perm[NMAX];          // LU row permutation: logical position -> physical row
+    int    pos[NMAX];           // its inverse: physical row -> logical position
+    double red[NW];
+    alignas(16) double L11[NB][NB + 1];    // unit-lower diagonal block of the current chunk
+    alignas(16) double Ub[NW][LU_CW][LU_CW];   // per wave: the chunk's pivot rows in its columns, then U;
+                                               // in its own panel: that chunk's pivot rows, saved at pivot time
+    double Pb[NW][LU_CW];                      // ... and their b
+    union alignas(16) {
+        double Lst[NB][NMAX];   // L of the current chunk by tile row, 0 where a row takes no update
+        double hist_acc[32];    // accel_step sums (used outside the LU only)
+    } pu;
+#endif
     // per-layer scalars
     double T, Te, vw, vgrad, nmol, ne;
     double cc[LVG_MAX_COMBOS];
@@ -197,6 +230,84 @@ struct LuSrc {
     const double *BK = nullptr, *BE = nullptr, *BD = nullptr;
 };
 
+// ---- back substitution U x = y in logical order, blocked by NB from the bottom:
+//      wave 0 solves the diagonal block in registers, then all threads update the
+//      rows above; every entry receives its updates for k descending (oracle order).
+//      b: LDS [N] by physical row; on return sm.blog holds x (logical = level order).
+__device__ __forceinline__ void back_substitute(const double *A, int N, const double *b, Smem &sm) {
+    const int t = threadIdx.x;
+    TSTAMP(tb0);
+    for (int i = t; i < N; i += BT) sm.blog[i] = b[sm.perm[i]];
+    __syncthreads();
+    const int nblk = (N + NB - 1) / NB;
+    // operands of block kb, loaded one block ahead so their latency hides behind the
+    // diagonal solve: the 16x16 diagonal block (one entry per thread) and the U
+    // segment U[perm[t]][k0..k0+nb) of this thread's row (rows above the block)
+    auto load_blk = [&](int kb, double &dv, double (&u)[NB]) {
+        const int k0 = kb * NB, nb = min(NB, N - k0);
+        const int r = t / NB, c = t - r * NB;
+        dv = (r < nb && c < nb) ? A[(int64_t)sm.perm[k0 + r] * N + k0 + c] : 0.;
+        const double *row = A + (int64_t)sm.perm[t < k0 ? t : 0] * N + k0;
+        if ((N & 1) == 0 && nb == NB) {
+            const double2 *r2 = reinterpret_cast<const double2 *>(row);
+#pragma unroll
+            for (int m = 0; m < NB / 2; m++) {
+                const double2 v = (t < k0) ? r2[m] : make_double2(0., 0.);
+                u[2 * m] = v.x;
+                u[2 * m + 1] = v.y;
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < NB; m++) u[m] = (t < k0 && m < nb) ? row[m] : 0.;
+        }
+    };
+    double dcur, ucur[NB], dnxt = 0., unxt[NB];
+    load_blk(nblk - 1, dcur, ucur);
+    for (int kb = nblk - 1; kb >= 0; kb--) {
+        const int k0 = kb * NB, nb = min(NB, N - k0);
+        {
+            const int r = t / NB, c = t - r * NB;
+            if (r < nb && c < nb) sm.L11[r][c] = dcur;
+        }
+        __syncthreads();
+        if (kb > 0) load_blk(kb - 1, dnxt, unxt);
+        if (t < 64) {
+            // diagonal block by wave 0 in registers: lane r < nb holds b_r and row r of the
+            // block; x_m (lane m's b_m / U_mm once final) is broadcast by DPP row_newbcast:m
+            const int r = t & 15;
+            double bt = (t < nb) ? sm.blog[k0 + t] : 0., ur[NB];
+#pragma unroll
+            for (int m = 0; m < NB; m++) ur[m] = (t < nb) ? sm.L11[r][m] : 1.;
+#define LVG_BSUB_STEP(M_)                                                                  \
+            if ((M_) < nb) {                                                               \
+                const double xm = dpp_d<0x150 + (M_), 0xf, 0xf>(bt / ur[M_]);              \
+                if (r < (M_)) bt = fma(-ur[M_], xm, bt);                                   \
+                else if (r == (M_)) bt = xm;                                               \
+            }
+            LVG_BSUB_STEP(15) LVG_BSUB_STEP(14) LVG_BSUB_STEP(13) LVG_BSUB_STEP(12)
+            LVG_BSUB_STEP(11) LVG_BSUB_STEP(10) LVG_BSUB_STEP(9) LVG_BSUB_STEP(8)
+            LVG_BSUB_STEP(7) LVG_BSUB_STEP(6) LVG_BSUB_STEP(5) LVG_BSUB_STEP(4)
+            LVG_BSUB_STEP(3) LVG_BSUB_STEP(2) LVG_BSUB_STEP(1) LVG_BSUB_STEP(0)
+#undef LVG_BSUB_STEP
+            if (t < nb) sm.blog[k0 + t] = bt;
+        }
+        __syncthreads();
+        if (t < k0) {
+            double s = sm.blog[t];
+#pragma unroll
+            for (int m = NB - 1; m >= 0; m--)
+                if (m < nb) s = fma(-ucur[m], sm.blog[k0 + m], s);
+            sm.blog[t] = s;
+        }
+        __syncthreads();
+        dcur = dnxt;
+#pragma unroll
+        for (int m = 0; m < NB; m++) ucur[m] = unxt[m];
+    }
+    TACC(PH_BACKSUB, tb0);
+}
+
+#if LVG_BIG
 // ------------------------------------------------------------------------------
 // Left-looking blocked LU with partial pivoting, b eliminated alongside.
 //
@@ -427,83 +538,6 @@ __device__ __forceinline__ void panel_factor_wave(double *A, int N, int kk, int 
         }
     }
     __syncthreads();
-}
-
-// ---- back substitution U x = y in logical order, blocked by NB from the bottom:
-//      wave 0 solves the diagonal block in registers, then all threads update the
-//      rows above; every entry receives its updates for k descending (oracle order).
-//      b: LDS [N] by physical row; on return sm.blog holds x (logical = level order).
-__device__ __forceinline__ void back_substitute(const double *A, int N, const double *b, Smem &sm) {
-    const int t = threadIdx.x;
-    TSTAMP(tb0);
-    for (int i = t; i < N; i += BT) sm.blog[i] = b[sm.perm[i]];
-    __syncthreads();
-    const int nblk = (N + NB - 1) / NB;
-    // operands of block kb, loaded one block ahead so their latency hides behind the
-    // diagonal solve: the 16x16 diagonal block (one entry per thread) and the U
-    // segment U[perm[t]][k0..k0+nb) of this thread's row (rows above the block)
-    auto load_blk = [&](int kb, double &dv, double (&u)[NB]) {
-        const int k0 = kb * NB, nb = min(NB, N - k0);
-        const int r = t / NB, c = t - r * NB;
-        dv = (r < nb && c < nb) ? A[(int64_t)sm.perm[k0 + r] * N + k0 + c] : 0.;
-        const double *row = A + (int64_t)sm.perm[t < k0 ? t : 0] * N + k0;
-        if ((N & 1) == 0 && nb == NB) {
-            const double2 *r2 = reinterpret_cast<const double2 *>(row);
-#pragma unroll
-            for (int m = 0; m < NB / 2; m++) {
-                const double2 v = (t < k0) ? r2[m] : make_double2(0., 0.);
-                u[2 * m] = v.x;
-                u[2 * m + 1] = v.y;
-            }
-        } else {
-#pragma unroll
-            for (int m = 0; m < NB; m++) u[m] = (t < k0 && m < nb) ? row[m] : 0.;
-        }
-    };
-    double dcur, ucur[NB], dnxt = 0., unxt[NB];
-    load_blk(nblk - 1, dcur, ucur);
-    for (int kb = nblk - 1; kb >= 0; kb--) {
-        const int k0 = kb * NB, nb = min(NB, N - k0);
-        {
-            const int r = t / NB, c = t - r * NB;
-            if (r < nb && c < nb) sm.L11[r][c] = dcur;
-        }
-        __syncthreads();
-        if (kb > 0) load_blk(kb - 1, dnxt, unxt);
-        if (t < 64) {
-            // diagonal block by wave 0 in registers: lane r < nb holds b_r and row r of the
-            // block; x_m (lane m's b_m / U_mm once final) is broadcast by DPP row_newbcast:m
-            const int r = t & 15;
-            double bt = (t < nb) ? sm.blog[k0 + t] : 0., ur[NB];
-#pragma unroll
-            for (int m = 0; m < NB; m++) ur[m] = (t < nb) ? sm.L11[r][m] : 1.;
-#define LVG_BSUB_STEP(M_)                                                                  \
-            if ((M_) < nb) {                                                               \
-                const double xm = dpp_d<0x150 + (M_), 0xf, 0xf>(bt / ur[M_]);              \
-                if (r < (M_)) bt = fma(-ur[M_], xm, bt);                                   \
-                else if (r == (M_)) bt = xm;                                               \
-            }
-            LVG_BSUB_STEP(15) LVG_BSUB_STEP(14) LVG_BSUB_STEP(13) LVG_BSUB_STEP(12)
-            LVG_BSUB_STEP(11) LVG_BSUB_STEP(10) LVG_BSUB_STEP(9) LVG_BSUB_STEP(8)
-            LVG_BSUB_STEP(7) LVG_BSUB_STEP(6) LVG_BSUB_STEP(5) LVG_BSUB_STEP(4)
-            LVG_BSUB_STEP(3) LVG_BSUB_STEP(2) LVG_BSUB_STEP(1) LVG_BSUB_STEP(0)
-#undef LVG_BSUB_STEP
-            if (t < nb) sm.blog[k0 + t] = bt;
-        }
-        __syncthreads();
-        if (t < k0) {
-            double s = sm.blog[t];
-#pragma unroll
-            for (int m = NB - 1; m >= 0; m--)
-                if (m < nb) s = fma(-ucur[m], sm.blog[k0 + m], s);
-            sm.blog[t] = s;
-        }
-        __syncthreads();
-        dcur = dnxt;
-#pragma unroll
-        for (int m = 0; m < NB; m++) ucur[m] = unxt[m];
-    }
-    TACC(PH_BACKSUB, tb0);
 }
 
 __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Smem &sm, const LuSrc &src, const bool FUSED) {
@@ -783,6 +817,10 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
     if (FUSED && t < N) { src.df[t] = s_acc; emax = fabs(s_acc); }
     return FUSED ? block_max(emax, sm) : 0.;
 }
+
+#else
+#include "lvg_lu256.h"
+#endif
 
 // ------------------------------------------------------------------------------
 // iteration_control (iteration_control.h:84-242)

@@ -1,5 +1,5 @@
 """Exactness probe for a library variant (LVG_LIB_PATH): a layer subset of a workload
-(default 128 CH3OH-A layers; argv: workload, layers) against the oracle."""
+(default 128 CH3OH-A layers; argv: workload, layers, levels) against the oracle."""
 import sys
 import numpy as np
 sys.path.insert(0, "/root/repo")
@@ -8,7 +8,8 @@ from oracle import oracle
 
 name = sys.argv[1] if len(sys.argv) > 1 else "ch3oha256_4096"
 nl = int(sys.argv[2]) if len(sys.argv) > 2 else 128
-P, L, o = synth.make_problem(name, nb_lay=nl)
+nlev = int(sys.argv[3]) if len(sys.argv) > 3 else None
+P, L, o = synth.make_problem(name, nb_lay=nl, nb_lev=nlev)
 opts = abi.default_opts(**o)
 s = native.LvgSolver(P)
 pg, sg = s.solve_layers(L, opts)
