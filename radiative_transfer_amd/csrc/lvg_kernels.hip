@@ -59,11 +59,8 @@ constexpr int NMAX = BT;                    // max levels of this kernel
 #ifndef LVG_OCC
 #define LVG_OCC (LVG_BIG ? 1 : 2)
 #endif
-#ifndef LVG_LU_CW
-#define LVG_LU_CW 16
-#endif
 constexpr int OCC  = LVG_OCC;               // resident workgroups per CU the kernel is built for
-constexpr int LU_CW = LVG_LU_CW;            // N <= 256 LU: columns per wave (lvg_lu256.h)
+constexpr int LU_CW = 16;                   // N <= 256 LU: columns per wave (lvg_lu256.h)
 constexpr int NW   = BT / 64;
 constexpr int NB   = 16;                    // LU panel width (chunk)
 static_assert(NMAX <= BT && BT % 64 == 0 && NMAX % 32 == 0, "one row per thread, whole waves");
@@ -108,9 +105,7 @@ struct Smem {
     int    pos[NMAX];           // its inverse: physical row -> logical position
     double red[NW];
     alignas(16) double L11[NB][NB + 1];    // unit-lower diagonal block of the current chunk
-    alignas(16) double Ub[NW][LU_CW][LU_CW];   // per wave: the chunk's pivot rows in its columns, then U;
-                                               // in its own panel: that chunk's pivot rows, saved at pivot time
-    double Pb[NW][LU_CW];                      // ... and their b
+    alignas(16) double Ub[NW][LU_CW][LU_CW];   // per wave: the chunk's pivot rows in its columns, then U
     union alignas(16) {
         double Lst[NB][NMAX];   // L of the current chunk by tile row, 0 where a row takes no update
         double hist_acc[32];    // accel_step sums (used outside the LU only)
