@@ -16,15 +16,21 @@ from radiative_transfer_amd import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "liblvg_oracle.so")
-# reference-arithmetic build (-DORACLE_REF_ARITH): glibc exp/log10/pow, LU without fma
-REF_LIB_PATH = os.path.join(HERE, "_build", "liblvg_oracle_ref.so")
+# reference-arithmetic builds: -DORACLE_REF_ARITH (glibc exp/log10/pow, LU without fma)
+# and one build per choice (-DORACLE_REF_EXP, _LU, _POW); ref= selects one by name
+REF_MASK = {False: 0, None: 0, True: 7, "all": 7, "exp": 1, "lu": 2, "pow": 4}
+REF_LIB = {0: LIB_PATH, 7: os.path.join(HERE, "_build", "liblvg_oracle_ref.so"),
+           1: os.path.join(HERE, "_build", "liblvg_oracle_ref_exp.so"),
+           2: os.path.join(HERE, "_build", "liblvg_oracle_ref_lu.so"),
+           4: os.path.join(HERE, "_build", "liblvg_oracle_ref_pow.so")}
+REF_LIB_PATH = REF_LIB[7]
 _libs = {}
 
 
 def _stale() -> bool:
-    if not (os.path.exists(LIB_PATH) and os.path.exists(REF_LIB_PATH)):
+    if not all(os.path.exists(p) for p in REF_LIB.values()):
         return True
-    t = min(os.path.getmtime(LIB_PATH), os.path.getmtime(REF_LIB_PATH))
+    t = min(os.path.getmtime(p) for p in REF_LIB.values())
     deps = [os.path.join(HERE, f) for f in ("lvg_oracle.c", "lvg_oracle.h", "Makefile")]
     deps += [os.path.join(HERE, "..", "include", f) for f in ("lvg_amd.h", "lvg_math.h")]
     return any(os.path.getmtime(x) > t for x in deps)
@@ -36,11 +42,13 @@ def build(force: bool = False) -> str:
     return LIB_PATH
 
 
-def lib(ref: bool = False):
-    """The bit-exact oracle, or with ref=True its reference-arithmetic build."""
-    if ref not in _libs:
+def lib(ref=False):
+    """The bit-exact oracle, or with ref=True its reference-arithmetic build; ref="exp",
+    "lu" or "pow" undoes that one choice only."""
+    mask = REF_MASK[ref]
+    if mask not in _libs:
         build()
-        L = C.CDLL(REF_LIB_PATH if ref else LIB_PATH)
+        L = C.CDLL(REF_LIB[mask])
         d, i, vp = C.c_double, C.c_int, C.c_void_p
         dp = C.POINTER(C.c_double)
         L.oracle_solve_layers.argtypes = [vp, vp, dp, vp, vp, i]
@@ -65,16 +73,16 @@ def lib(ref: bool = False):
         L.oracle_log10.argtypes = [d]
         L.oracle_log10.restype = d
         L.oracle_ref_arith.restype = i
-        assert L.oracle_ref_arith() == int(ref)
-        _libs[ref] = L
-    return _libs[ref]
+        assert L.oracle_ref_arith() == mask
+        _libs[mask] = L
+    return _libs[mask]
 
 
 def _nz(a):
     return abi.dptr(a) if a is not None else None
 
 
-def solve_layers(prob: abi.Problem, layers: abi.Layers, opts=None, pops=None, nthreads: int = 0, ref: bool = False):
+def solve_layers(prob: abi.Problem, layers: abi.Layers, opts=None, pops=None, nthreads: int = 0, ref=False):
     cp, cl = prob.to_c(), layers.to_c()
     N = prob.mol.nb_lev
     o = opts if opts is not None else abi.default_opts()
@@ -87,7 +95,7 @@ def solve_layers(prob: abi.Problem, layers: abi.Layers, opts=None, pops=None, nt
     return out, st
 
 
-def solve_chains(prob: abi.Problem, layers: abi.Layers, chain_off, opts=None, nthreads: int = 0, ref: bool = False):
+def solve_chains(prob: abi.Problem, layers: abi.Layers, chain_off, opts=None, nthreads: int = 0, ref=False):
     """oracle_solve_chains: independent warm chains [chain_off[c], chain_off[c+1])."""
     cp, cl = prob.to_c(), layers.to_c()
     o = opts if opts is not None else abi.default_opts(init=abi.LVG_INIT_WARM_CHAIN)
@@ -101,7 +109,7 @@ def solve_chains(prob: abi.Problem, layers: abi.Layers, chain_off, opts=None, nt
     return out, st
 
 
-def calc_new_pop(prob, layers, layer, pop_in, overlap=0, ref: bool = False):
+def calc_new_pop(prob, layers, layer, pop_in, overlap=0, ref=False):
     cp, cl = prob.to_c(), layers.to_c()
     N = prob.mol.nb_lev
     pin = np.ascontiguousarray(pop_in, dtype=np.float64)
@@ -112,7 +120,7 @@ def calc_new_pop(prob, layers, layer, pop_in, overlap=0, ref: bool = False):
     return M, df, pout, e.value
 
 
-def boundary_layer_populations(prob, layers, ref: bool = False):
+def boundary_layer_populations(prob, layers, ref=False):
     cp, cl = prob.to_c(), layers.to_c()
     out = np.zeros((layers.nb_lay, prob.mol.nb_lev))
     lib(ref).oracle_boundary_layer_populations(cp.ptr, cl.ptr, abi.dptr(out))
