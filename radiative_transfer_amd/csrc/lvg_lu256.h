@@ -142,33 +142,57 @@ __device__ __forceinline__ void lu2_panel(double (&acc)[S4][CW], const int (&pro
 #pragma clang loop unroll(full)
     for (int c = 0; c < CW; c++) {
         if (c < nb) {
-            unsigned bh = 0u, bl = 0u;
-            int bp = 0x7fffffff, bs = 0;
+            // fast path: upper words only (|v|'s sign bit replaced by the active flag), the
+            // lane's best of its slots, one wave max, one ballot per slot. It decides when
+            // exactly one row carries the maximum upper word and that word is finite (an inf
+            // or NaN among the active rows puts it at 0xfff00000 or above); a tie in the
+            // upper word, an inf or a NaN takes the full key (lower word, then the first
+            // logical position, NaN diagonal), so the pivot is the oracle's in every case.
+            unsigned kh[S4];
 #pragma unroll
-            for (int s = 0; s < S4; s++) {
-                if (s >= s_lo) {
-                    unsigned hi, lo;
-                    pivot_key(acc[s][c], act[s], lp[s] == c, hi, lo);
-                    const bool better = hi > bh || (hi == bh && (lo > bl || (lo == bl && (unsigned)lp[s] < (unsigned)bp)));
-                    bh = better ? hi : bh;
-                    bl = better ? lo : bl;
-                    bp = better ? lp[s] : bp;
-                    bs = better ? s : bs;
-                }
-            }
-            const unsigned H = wave_max_u32(bh);
-            const unsigned long long tie = __ballot(bh == H);
-            int pl;
-            if (__popcll(tie) == 1) {
-                pl = __ffsll((long long)tie) - 1;
+            for (int s = 0; s < S4; s++)
+                kh[s] = (s >= s_lo && act[s]) ? ((unsigned)__double2hiint(acc[s][c]) | 0x80000000u) : 0u;
+            const unsigned H0 = wave_max_u32(max(max(kh[0], kh[1]), max(kh[2], kh[3])));
+            unsigned long long mk[S4];
+            int cnt = 0;
+#pragma unroll
+            for (int s = 0; s < S4; s++) { mk[s] = __ballot(kh[s] == H0); cnt += __popcll(mk[s]); }
+            int pl, ss, plp;
+            if (H0 < 0xfff00000u && cnt == 1) {
+                ss = mk[0] ? 0 : mk[1] ? 1 : mk[2] ? 2 : 3;
+                pl = __builtin_amdgcn_readfirstlane(__ffsll((long long)(mk[0] | mk[1] | mk[2] | mk[3])) - 1);
+                int lps = lp[0];
+#pragma unroll
+                for (int s = 1; s < S4; s++) lps = ss == s ? lp[s] : lps;
+                plp = __builtin_amdgcn_readlane(lps, pl);
             } else {
-                const unsigned Lw = wave_max_u32(bh == H ? bl : 0u);
-                const unsigned X = wave_max_u32((bh == H && bl == Lw) ? ~(unsigned)bp : 0u);
-                pl = __ffsll((long long)__ballot(bh == H && bl == Lw && bp == (int)~X)) - 1;
+                unsigned bh = 0u, bl = 0u;
+                int bp = 0x7fffffff, bs = 0;
+#pragma unroll
+                for (int s = 0; s < S4; s++) {
+                    if (s >= s_lo) {
+                        unsigned hi, lo;
+                        pivot_key(acc[s][c], act[s], lp[s] == c, hi, lo);
+                        const bool better = hi > bh || (hi == bh && (lo > bl || (lo == bl && (unsigned)lp[s] < (unsigned)bp)));
+                        bh = better ? hi : bh;
+                        bl = better ? lo : bl;
+                        bp = better ? lp[s] : bp;
+                        bs = better ? s : bs;
+                    }
+                }
+                const unsigned H = wave_max_u32(bh);
+                const unsigned long long tie = __ballot(bh == H);
+                if (__popcll(tie) == 1) {
+                    pl = __ffsll((long long)tie) - 1;
+                } else {
+                    const unsigned Lw = wave_max_u32(bh == H ? bl : 0u);
+                    const unsigned X = wave_max_u32((bh == H && bl == Lw) ? ~(unsigned)bp : 0u);
+                    pl = __ffsll((long long)__ballot(bh == H && bl == Lw && bp == (int)~X)) - 1;
+                }
+                pl = __builtin_amdgcn_readfirstlane(pl);
+                ss = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(bs, pl));
+                plp = __builtin_amdgcn_readlane(bp, pl);
             }
-            pl = __builtin_amdgcn_readfirstlane(pl);
-            const int ss = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(bs, pl));
-            const int plp = __builtin_amdgcn_readlane(bp, pl);
             double pr[CW], bc;
             {
                 double sv[CW], sb = rb[0];
