@@ -337,6 +337,13 @@ int         lvg_last_kernel_time(const lvg_handle *h, double *ms, int *nb_launch
  * (coll_rates.cpp:152-174, iteration_lvg.cpp:121-131); no reference counterpart. */
 int         lvg_last_coll_time(const lvg_handle *h, double *ms);
 
+/* Which solve kernel ran the last lvg_solve_* call on this handle (diagnostic; every
+ * kernel gives bit-identical results): 0 the 256-thread block kernel (N <= 256), 1 the
+ * wave kernel (N <= 64), 2 the 512-thread block kernel (N <= 256, launches with at most
+ * two independent layers or one warm chain per CU), 3 the 768-thread block kernel
+ * (N > 256). No reference counterpart. */
+int         lvg_last_kernel_kind(const lvg_handle *h, int *kind);
+
 /* Tuning and diagnostics of this handle: "key=value,key=value" (NULL or "" = the
  * defaults); the environment variable LVG_TUNING supplies the initial value at
  * lvg_create. No setting changes a result (populations and status stay bit-identical).

@@ -37,6 +37,9 @@ extern "C" int lvg_kernel_max_levels(void);
 extern "C" hipError_t lvg_kernel_occupancy(int *blocks_per_cu);
 extern "C" hipError_t lvg_launch_lum(const LvgDevProblem *P, const LvgLaunch *L, const LvgLumArgs *A, int grid,
                                      int nb_trans, int nb_lay, hipStream_t s);
+// the 512-thread instantiation for underfilled launches at N <= 256 (lvg_kernels_wide.hip)
+extern "C" hipError_t lvg_launch_solve_wide(const LvgDevProblem *P, const LvgLaunch *L, int grid, hipStream_t s);
+extern "C" hipError_t lvg_kernel_occupancy_wide(int *blocks_per_cu);
 // the 768-thread instantiation for 256 < N <= 768 (lvg_kernels_big.hip)
 extern "C" hipError_t lvg_launch_solve_big(const LvgDevProblem *P, const LvgLaunch *L, int grid, hipStream_t s);
 extern "C" hipError_t lvg_launch_debug_big(const LvgDevProblem *P, const LvgLaunch *L, hipStream_t s);
@@ -75,6 +78,7 @@ struct LvgTuning {
     double coll_mem = 0.5;     // coll_mem=f: ... when they fit this fraction of the free device memory
     int coll_order = 1;        // coll_order=0: coll_kernel in layer order, not temperature order
     int blocks_per_cu = 0;     // blocks_per_cu=k: resident block-kernel workgroups per CU (0: automatic)
+    int wide = 1;              // wide=0: never the 512-thread kernel; 1: when underfilled; 2: always (N <= 256)
 };
 
 struct lvg_handle {
@@ -83,6 +87,7 @@ struct lvg_handle {
     int nb_comp = 0;
     int has_overlap = 0;
     int cus = 0, blocks_per_cu = 1;
+    int wide_bpc = 0;              // resident 512-thread workgroups per CU (0: not available)
     int big = 0;                   // N > 256: the 768-thread block kernel (lvg_kernels_big.hip)
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evc = nullptr;   // evc: end of coll_kernel
@@ -94,7 +99,7 @@ struct lvg_handle {
     int64_t ws_stride = 0;
     int *counter = nullptr;
     size_t lds_cap = 0;            // LDS bytes per workgroup (wave kernel plan)
-    int last_kernel = 0;           // 0 block kernel, 1 wave kernel (last solve)
+    int last_kernel = 0;           // lvg_last_kernel_kind: 0 block, 1 wave, 2 512-thread, 3 768-thread kernel
     // scratch for host-buffer solves
     double *d_soa = nullptr, *d_pops = nullptr;
     void *d_status = nullptr;
@@ -162,6 +167,7 @@ int parse_tuning(lvg_handle *h, const char *spec, LvgTuning &t) {
         else if (k == "coll_mem" && x >= 0. && x <= 1.) t.coll_mem = x;
         else if (k == "coll_order") t.coll_order = x != 0.;
         else if (k == "blocks_per_cu" && x >= 0. && x <= 8.) t.blocks_per_cu = (int)x;
+        else if (k == "wide" && (x == 0. || x == 1. || x == 2.)) t.wide = (int)x;
         else return fail(h, LVG_E_ARG, "unknown tuning key or bad value '%s'", item.c_str());
     }
     return LVG_OK;
@@ -799,6 +805,8 @@ int lvg_create(const lvg_problem *prob, int device, lvg_handle **out) {
             h->big = h->N > lvg_kernel_max_levels();
             if ((h->big ? lvg_kernel_occupancy_big(&b) : lvg_kernel_occupancy(&b)) != hipSuccess || b < 1) b = 1;
             h->blocks_per_cu = b;
+            int bw = 0;
+            if (!h->big && lvg_kernel_occupancy_wide(&bw) == hipSuccess) h->wide_bpc = std::min(bw, 1);
         }
     }
     if (rc != LVG_OK) {
@@ -859,10 +867,17 @@ int launch_solve(lvg_handle *h, int nb_lay, const double *d_soa, double *d_pops,
         }
     }
     const bool wave = wpb > 0;
+    // the 512-thread kernel (lvg_kernels_wide.hip, N <= 256) when the launch leaves CUs to
+    // spare: at most two independent layers or one warm chain per CU. There one layer's
+    // latency is the step, and eight waves per layer give every SIMD two waves to switch
+    // between and halve each wave's update work. Bit-identical results.
+    const bool wide = !wave && !h->big && h->wide_bpc >= 1 &&
+                      (h->tune.wide == 2 || (h->tune.wide == 1 && nq <= (chain_off ? 1 : 2) * h->cus));
     const int grid = wave ? std::max(1, std::min((nq + wpb - 1) / wpb, h->cus * wave_bpc))
+                   : wide ? std::max(1, std::min(nq, h->cus * h->wide_bpc))
                           : std::max(1, std::min(nq, h->cus * per_cu));
     const int slots = wave ? grid * wpb : grid;
-    h->last_kernel = wave ? 1 : 0;
+    h->last_kernel = wave ? 1 : wide ? 2 : h->big ? 3 : 0;
     if ((rc = ensure_workspace(h, slots))) return rc;
     LvgLaunch L;
     fill_launch(h, L, o);
@@ -954,6 +969,7 @@ int launch_solve(lvg_handle *h, int nb_lay, const double *d_soa, double *d_pops,
         HIPCHECK(h, hipEventRecord(h->evc, s));
     }
     if (wave) HIPCHECK(h, lvg_launch_solve_wave(h->d_prob, dL, h->N, grid, wpb, wdyn, s));
+    else if (wide) HIPCHECK(h, lvg_launch_solve_wide(h->d_prob, dL, grid, s));
     else HIPCHECK(h, h->big ? lvg_launch_solve_big(h->d_prob, dL, grid, s) : lvg_launch_solve(h->d_prob, dL, grid, s));
     HIPCHECK(h, hipEventRecord(h->ev1, s));
     h->last_launches = 1;
@@ -1027,6 +1043,13 @@ int lvg_last_coll_time(const lvg_handle *h, double *ms) {
     int rc = lvg_last_kernel_time(h, &k, nullptr);   // settles both timings
     if (rc) return rc;
     if (ms) *ms = h->last_coll ? h->last_coll_ms : 0.;
+    return LVG_OK;
+}
+
+int lvg_last_kernel_kind(const lvg_handle *h, int *kind) {
+    if (!h) return LVG_E_STATE;
+    if (!kind) return LVG_E_ARG;
+    *kind = h->last_kernel;
     return LVG_OK;
 }
 

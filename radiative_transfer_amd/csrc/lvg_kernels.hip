@@ -16,13 +16,15 @@
 // only fused multiply-adds are the explicit fma() of the LU, whose per-element update
 // sequence (k ascending) the blocked factorization preserves.
 //
-// Instantiation. The product library compiles this file twice: as is (namespace lvg,
-// 256 threads, N <= 256, 2 workgroups per CU) and through lvg_kernels_big.hip (LVG_BIG:
-// namespace lvg_big, 768 threads, N <= 768 — the reference's CH3OH callers,
-// radiative_transfer.cpp:647, :773 — one workgroup per CU, the whole LDS). The
-// algorithm, the operation order and hence the results are the same; every extern "C"
-// entry of the second copy carries the suffix _big. The wave-per-layer kernel for
-// N <= 64 is lvg_wave.hip.
+// Instantiation. The product library compiles this file three times: as is (namespace
+// lvg, 256 threads, N <= 256, 2 workgroups per CU), through lvg_kernels_wide.hip
+// (LVG_WIDE: namespace lvg_wide, 512 threads, N <= 256, one workgroup per CU — for
+// launches with at most two layers or one chain per CU, where one layer's latency is the
+// step) and through lvg_kernels_big.hip (LVG_BIG: namespace lvg_big, 768 threads,
+// N <= 768 — the reference's CH3OH callers, radiative_transfer.cpp:647, :773 — one
+// workgroup per CU, the whole LDS). The algorithm, the operation order and hence the
+// results are the same; every extern "C" entry of the other copies carries the suffix
+// _wide / _big. The wave-per-layer kernel for N <= 64 is lvg_wave.hip.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
@@ -34,9 +36,15 @@
 #ifndef LVG_BIG
 #define LVG_BIG 0
 #endif
+#ifndef LVG_WIDE
+#define LVG_WIDE 0
+#endif
 #if LVG_BIG
 #define LVG_NS lvg_big
 #define LVG_SYM(name) name##_big
+#elif LVG_WIDE
+#define LVG_NS lvg_wide
+#define LVG_SYM(name) name##_wide
 #else
 #define LVG_NS lvg
 #define LVG_SYM(name) name
@@ -54,16 +62,16 @@ namespace LVG_NS {
     atomicAdd(&lvg_ph_lds[ph], t_ - (v0)); } } while (0)
 #endif
 
-constexpr int BT   = LVG_BIG ? 768 : 256;   // threads per workgroup (one panel row per thread: N <= BT)
-constexpr int NMAX = BT;                    // max levels of this kernel
+constexpr int BT   = LVG_BIG ? 768 : LVG_WIDE ? 512 : 256;   // threads per workgroup
+constexpr int NMAX = LVG_BIG ? 768 : 256;   // max levels of this kernel
 #ifndef LVG_OCC
-#define LVG_OCC (LVG_BIG ? 1 : 2)
+#define LVG_OCC (LVG_BIG || LVG_WIDE ? 1 : 2)
 #endif
 constexpr int OCC  = LVG_OCC;               // resident workgroups per CU the kernel is built for
 constexpr int LU_CW = 16;                   // N <= 256 LU: columns per wave (lvg_lu256.h)
 constexpr int NW   = BT / 64;
 constexpr int NB   = 16;                    // LU panel width (chunk)
-static_assert(NMAX <= BT && BT % 64 == 0 && NMAX % 32 == 0, "one row per thread, whole waves");
+static_assert(NMAX <= BT && BT % 64 == 0 && NMAX % 32 == 0, "at least one row per thread, whole waves");
 constexpr int YCAP = LVG_BIG ? 1 : 2048;    // line terms kept in LDS when 2*nb_lines <= YCAP
 constexpr int TC = 4;                       // columns per thread in the LU register tile (TR rows x TC)
 constexpr int TR = NMAX * 8 / BT;           // tile rows per thread: the BT/8 row groups cover NMAX
@@ -1172,7 +1180,7 @@ __global__ void __launch_bounds__(64) lum_reduce_kernel(const LvgLumArgs *__rest
     A.lum[tr] = s / A.height;
 }
 
-#if !LVG_BIG
+#if !LVG_BIG && !LVG_WIDE
 // ---- collision operators of a whole batch of layers, ahead of the solve ----------------
 // build_collision_operators for every layer of the launch into K_all / B_all (HBM), with
 // a small LDS footprint (layer scalars and the rule table only) so that many workgroups
@@ -1252,7 +1260,7 @@ extern "C" hipError_t LVG_SYM(lvg_launch_solve)(const LvgDevProblem *P, const Lv
     return hipGetLastError();
 }
 
-#if !LVG_BIG
+#if !LVG_BIG && !LVG_WIDE
 extern "C" hipError_t lvg_launch_coll(const LvgDevProblem *P, const LvgLaunch *L, int grid, hipStream_t s) {
     hipLaunchKernelGGL(lvg::coll_kernel, dim3(grid), dim3(lvg::BT), 0, s, P, L);
     return hipGetLastError();

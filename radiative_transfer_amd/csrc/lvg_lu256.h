@@ -4,7 +4,8 @@
 // lu_matrix_solve (absent library; call sites iteration_lvg.cpp:100, iteration_control.cpp:87)
 // as a left-looking blocked LU with partial pivoting, b eliminated alongside, in which
 // every wave OWNS COLUMNS:
-//  * Block columns of 64; wave w holds columns c0 + 16w .. c0 + 16w + 15 of every row in
+//  * Block columns of 16 x (waves): 64 for the 256-thread kernel, 128 for the 512-thread
+//    one (LVG_WIDE); wave w holds columns c0 + 16w .. c0 + 16w + 15 of every row in
 //    registers: lane l keeps tile rows 64 s + l (s < 4, logical order as of the block
 //    load), acc[s][0..16) — 128 fp64 registers.
 //  * An earlier chunk kk (16 columns of L, final) is staged once per workgroup into LDS
@@ -27,7 +28,7 @@
 
 constexpr int S4 = NMAX / 64;   // row slots per lane: tile row 64 s + lane
 constexpr int CW = LU_CW;       // columns per wave = chunk (panel) width: 16 or 8
-constexpr int BW = 4 * CW;      // block-column width
+constexpr int BW = NW * CW;     // block-column width: 64 (4 waves) or 128 (8 waves, LVG_WIDE)
 constexpr int CL = CW / 4;      // TRSM columns per lane (4 x 16-lane rows)
 static_assert(CW == 16, "chunk width: the TRSM and the panel assume 16 columns per wave");
 

@@ -21,7 +21,7 @@ EXPORTS = ("lvg_abi_version", "lvg_solve_opts_default", "lvg_create", "lvg_destr
            "lvg_nb_lev", "lvg_solve_layers", "lvg_layer_soa_rows", "lvg_solve_layers_device",
            "lvg_debug_calc_new_pop", "lvg_boundary_layer_populations", "lvg_find_opts_default",
            "lvg_find_transitions", "lvg_lim_luminosity", "lvg_last_kernel_time", "lvg_solve_chains",
-           "lvg_solve_chains_device", "lvg_last_coll_time", "lvg_set_tuning")
+           "lvg_solve_chains_device", "lvg_last_coll_time", "lvg_set_tuning", "lvg_last_kernel_kind")
 
 _lib = None
 
@@ -56,6 +56,7 @@ def load(path: str = LIB_PATH):
     L.lvg_last_kernel_time.argtypes = [vp, dp, C.POINTER(C.c_int)]
     L.lvg_last_coll_time.argtypes = [vp, dp]
     L.lvg_set_tuning.argtypes = [vp, C.c_char_p]
+    L.lvg_last_kernel_kind.argtypes = [vp, C.POINTER(C.c_int)]
     L.lvg_find_opts_default.argtypes = [vp]
     ip = C.POINTER(C.c_int)
     L.lvg_lim_luminosity.argtypes = [vp, vp, vp, dp, i, ip, ip, i, dp, dp, dp, dp, dp, dp]
@@ -158,6 +159,13 @@ class LvgSolver:
         ms = C.c_double()
         self._check(self.lib.lvg_last_coll_time(self.h, C.byref(ms)), "lvg_last_coll_time")
         return ms.value
+
+    def last_kernel_kind(self):
+        """The solve kernel of the last solve: 0 block (256 threads), 1 wave, 2 block (512
+        threads, underfilled launches), 3 block (768 threads, N > 256)."""
+        k = C.c_int()
+        self._check(self.lib.lvg_last_kernel_kind(self.h, C.byref(k)), "lvg_last_kernel_kind")
+        return k.value
 
     def debug_calc_new_pop(self, layers: abi.Layers, layer: int, pop_in, overlap: int = 0):
         cl = layers.to_c()

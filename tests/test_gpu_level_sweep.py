@@ -2,9 +2,9 @@
 
 The kernel selected and its register tiling depend on N: the wave kernel's NM = 16..64
 instantiations (one per 8 levels, lvg_wave.h), the 256-thread block kernel's panel paths
-around the 64-row wave boundaries (4-wave panel, one wave taking two rows per lane, one
-wave alone; lvg_kernels.hip block_lu_solve) and the 768-thread instantiation for
-256 < N <= 768 (lvg_kernels_big.hip). Each N here is solved on a few layers from the
+around its 64- and 128-column block boundaries, both the 256-thread instantiation (4 waves,
+64-column blocks) and the 512-thread one (8 waves, 128-column blocks; lvg_kernels_wide.hip,
+lvg_lu256.h), and the 768-thread instantiation for 256 < N <= 768 (lvg_kernels_big.hip). Each N here is solved on a few layers from the
 boundary-layer start (radiative_transfer.cpp:236-288) with acceleration on, and the
 boundary-layer solve (iteration_control.cpp:52-91) is compared on its own.
 """
@@ -19,15 +19,19 @@ from parity_helpers import assert_same
 pytestmark = pytest.mark.gpu
 
 WAVE_N = [20, 28, 40, 52, 60]                       # NM = 24, 32, 40, 56, 64
-BLOCK_N = [65, 96, 128, 129, 192, 193, 240, 255]    # wave boundaries of the 256-thread kernel
+BLOCK_N = [65, 96, 128, 129, 192, 193, 240, 255]    # 64-row slot and 64/128-column block boundaries
 BIG_N = [320, 385, 512, 640]                        # 768-thread kernel
 
 
-def _run(name, nlev, nl):
+def _run(name, nlev, nl, tuning="", kind=None):
     P, L, o = synth.make_problem(name, nb_lay=nl, nb_lev=nlev)
     opts = abi.default_opts(**{**o, "accel_nb": 3, "accel_start": 3, "accel_period": 2})
     s = LvgSolver(P)
+    if tuning:
+        s.set_tuning(tuning)
     pg, sg = s.solve_layers(L, opts)
+    if kind is not None:
+        assert s.last_kernel_kind() == kind
     po, so = oracle.solve_layers(P, L, opts)
     assert_same(pg, sg, po, so)
     assert np.array_equal(s.boundary_layer_populations(L), oracle.boundary_layer_populations(P, L))
@@ -40,10 +44,11 @@ def test_wave_level_counts(nlev):
 
 
 @pytest.mark.parametrize("nlev", BLOCK_N)
-def test_block_level_counts(nlev):
-    _run("ch3oha256_4096", nlev, 4)
+@pytest.mark.parametrize("wide", [0, 2])
+def test_block_level_counts(nlev, wide):
+    _run("ch3oha256_4096", nlev, 4, f"wide={wide}", 2 if wide else 0)
 
 
 @pytest.mark.parametrize("nlev", BIG_N)
 def test_big_level_counts(nlev):
-    _run("ch3oha256_4096", nlev, 2)
+    _run("ch3oha256_4096", nlev, 2, kind=3)

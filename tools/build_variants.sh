@@ -10,9 +10,12 @@ pids=()
 for spec in "$@"; do
   k=${spec%%:*}; rest=${spec#*:}; src=${rest%%:*}; flags=${rest#*:}
   [ "$src" = "$rest" ] && flags=""
-  case "$(basename $src)" in
-    *wave*) objs="$O/lvg_kernels.o $O/var_$k.o" ;;
-    *)      objs="$O/var_$k.o $O/lvg_wave.o" ;;
+  # the variant object replaces the product object of its kind: the wave kernel, the
+  # 512-thread instantiation (flags with -DLVG_WIDE=1) or the 256-thread one
+  case "$(basename $src) $flags" in
+    *wave*)         objs="$O/lvg_kernels.o $O/lvg_kernels_wide.o $O/var_$k.o" ;;
+    *LVG_WIDE=1*)   objs="$O/lvg_kernels.o $O/var_$k.o $O/lvg_wave.o" ;;
+    *)              objs="$O/var_$k.o $O/lvg_kernels_wide.o $O/lvg_wave.o" ;;
   esac
   ( /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I radiative_transfer_amd/csrc $flags \
       -c $src -o $O/var_$k.o &&

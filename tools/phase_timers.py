@@ -20,11 +20,22 @@ P, L, o = synth.make_problem(name, nb_lay=nl)
 s = native.LvgSolver(P)
 lib = native.load()
 buf = (C.c_ulonglong * 32)()
+
+
+def read_counters(out, reset):
+    """256- and 512-thread kernels' counters summed (one kind runs per launch)."""
+    a, b = (C.c_ulonglong * 32)(), (C.c_ulonglong * 32)()
+    lib.lvg_debug_phase_cycles(a, reset)
+    lib.lvg_debug_phase_cycles_wide(b, reset)
+    for i in range(32):
+        out[i] = a[i] + b[i]
+
+
 s.solve_layers(L, abi.default_opts(**o))
-lib.lvg_debug_phase_cycles(buf, 1)
+read_counters(buf, 1)
 t = time.time(); pops, st = s.solve_layers(L, abi.default_opts(**o)); dt = time.time() - t
 ms, _ = s.last_kernel_time()
-lib.lvg_debug_phase_cycles(buf, 1)
+read_counters(buf, 1)
 cyc = np.array(buf[:32], dtype=np.float64)
 clk = np.array(buf[13:15], dtype=np.float64)
 its = st["iterations"].sum()
