@@ -289,6 +289,9 @@ class StubSolver:
     def last_coll_time(self):
         return 0.0
 
+    def last_kernel_kind(self):
+        return 0
+
     def close(self):
         pass
 
@@ -388,6 +391,7 @@ def run_rank(args) -> int:
         td.barrier()
     elapsed = time.perf_counter() - t0
     prov_rec = prov.timed_end()
+    kernel_kind = solver.last_kernel_kind() if n_mine > 0 else 0
     st2 = dist.status_numpy(status[:n_mine])
     assert int(st2["iterations"].sum()) == units_local, "iteration count changed between steps"
     if multi:
@@ -411,7 +415,7 @@ def run_rank(args) -> int:
     if rank == 0:
         print(json.dumps(report(args, world, N, total, L_cfg, lo, hi, units_total, units_local, nonconv, max_rel,
                                 max_layer_its, elapsed, kern_ms, coll_ms, opts, offs, prov_rec, host_value,
-                                prob, mine, stub)), flush=True)
+                                prob, mine, stub, kernel_kind)), flush=True)
     solver.close()
     if multi:
         td.destroy_process_group()
@@ -419,13 +423,15 @@ def run_rank(args) -> int:
 
 
 def report(args, world, N, total, L_cfg, lo, hi, units_total, units_local, nonconv, max_rel, max_layer_its,
-           elapsed, kern_ms, coll_ms, opts, offs, prov_rec, host_value, prob, mine, stub):
+           elapsed, kern_ms, coll_ms, opts, offs, prov_rec, host_value, prob, mine, stub, kernel_kind=0):
     from radiative_transfer_amd import synth
     value = units_total * args.steps / elapsed
     kms = float(np.mean(kern_ms))
     cms = float(np.mean(coll_ms))
     ms_step = 1e3 * elapsed / args.steps
-    kernel = "lvg::solve_wave_kernel" if N <= 64 else "lvg::solve_kernel" if N <= 256 else "lvg_big::solve_kernel"
+    # the kernel the ABI chose for this launch (lvg_last_kernel_kind)
+    kernel = {0: "lvg::solve_kernel", 1: "lvg::solve_wave_kernel", 2: "lvg_wide::solve_kernel",
+              3: "lvg_big::solve_kernel"}[kernel_kind]
     bound = binding_roof(N)
     per_launch = units_local
     F, B = flops_per_layer_iteration(N), bytes_per_layer_iteration(N)
@@ -469,7 +475,10 @@ def report(args, world, N, total, L_cfg, lo, hi, units_total, units_local, nonco
         "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
         "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (synth_v1, SURVEY.md 8d)" + (" [STUB solver: launcher test]" if stub else ""),
-        "config": {"workload": args.workload, "nb_lev": N, "layers_total": total,
+        # a level or layer count other than the config's is named in the workload label
+        "config": {"workload": args.workload + (f"_nblev{N}" if N != synth.CONFIGS[args.workload][1] else "")
+                   + (f"_layers{args.layers}" if args.layers and args.layers != L_cfg else ""),
+                   "nb_lev": N, "layers_total": total,
                    "layers_per_gpu": layers_rank if world == 1 or not args.strong
                    else f"{total // world}-{-(-total // world)}",
                    "layer_iterations_per_step": units_total, "nonconverged_layers": nonconv,

@@ -9,7 +9,7 @@ tag = sys.argv[1] if len(sys.argv) > 1 else "r1"
 workload = sys.argv[2] if len(sys.argv) > 2 else "ch3oha256_4096"
 src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}_{workload}")
 dst = os.path.join(ROOT, "profiles", tag, workload)
-KERNELS = ("solve_kernel", "solve_wave_kernel")
+KERNELS = ("lvg::solve_kernel", "lvg_wide::solve_kernel", "lvg_big::solve_kernel", "solve_wave_kernel")
 os.makedirs(dst, exist_ok=True)
 
 
@@ -47,6 +47,7 @@ data[workload] = {
     "correction": "MI355X_MICROARCH.md §HBM: FETCH_SIZE counts 1/2 of the bytes of wide coalesced reads on gfx950 -> doubled; WRITE_SIZE taken as is; bytes = kB*1024",
     "units_per_launch": bj["config"]["layer_iterations_per_step"],
     "source": f"profiles/{tag}/{workload}/pmc_fetch_solve_kernel.csv, pmc_write_solve_kernel.csv (rocprofv3 --pmc, separate passes)",
+    "commit": open(os.path.join(ROOT, ".commit")).read().strip() if os.path.exists(os.path.join(ROOT, ".commit")) else "?",
 }
 json.dump(data, open(p, "w"), indent=1)
 print(json.dumps(data[workload], indent=1))
