@@ -8,7 +8,7 @@ TAG=${1:-r2}
 WL=${2:-ch3oha256_4096}
 OUT=gpurun_out/prof_${TAG}_${WL}
 mkdir -p $OUT
-B="python3 bench.py --workload $WL --no-cpu --no-host-entry"
+B="python3 bench.py --workload $WL --no-cpu --no-host-entry --no-provenance"   # no rocm-smi child under the profiler
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
     $B --steps 3 --warmup 1 > $OUT/bench_trace.json 2> $OUT/trace.err && \
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- \
