@@ -76,5 +76,4 @@ def compare(name: str, nb: int | None = None, nthreads: int = 0):
 
 if __name__ == "__main__":
     import json
-    for n in SAMPLES:
-        print(json.dumps(compare(n)))
+    print(json.dumps([compare(n) for n in SAMPLES], indent=1))
