@@ -103,12 +103,18 @@ __device__ __forceinline__ void lu2_apply(double (&acc)[S4][CW], const int (&pro
         const double2 *up = reinterpret_cast<const double2 *>(&Ub[m][0]);
 #pragma unroll
         for (int j = 0; j < CW / 2; j++) { const double2 v = up[j]; u[2 * j] = v.x; u[2 * j + 1] = v.y; }
+        // every slot's L read with the U row (one LDS wait per m, not one per slot): the
+        // asm use keeps the reads from being sunk into the slot branches
+        double a[S4];
+#pragma unroll
+        for (int s = 0; s < S4; s++) a[s] = sm.pu.Lst[m][64 * s + l];
+        static_assert(S4 == 4, "four row slots");
+        asm volatile("" :: "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]));
 #pragma unroll
         for (int s = 0; s < S4; s++) {
             if (s >= s_lo) {
-                const double a = sm.pu.Lst[m][64 * s + l];
 #pragma unroll
-                for (int c = 0; c < CW; c++) acc[s][c] = fma(-a, u[c], acc[s][c]);
+                for (int c = 0; c < CW; c++) acc[s][c] = fma(-a[s], u[c], acc[s][c]);
             }
         }
     }
