@@ -61,7 +61,7 @@ struct WaveShared {               // per-block LDS (static part)
     WaveLayer w[4];
 };
 
-// dynamic LDS: line index map [N][N|1] (int), then K [wpb][N][N|1] (double)
+// dynamic LDS: line index map [NM][NM|1] (int), then K [wpb][NM][NM|1] (double); rows N..NM-1 unused
 extern __shared__ double lvg_wave_dyn[];
 
 // LDS stores of one lane become visible to the other lanes of its wave (workgroup-scope
@@ -85,7 +85,7 @@ __device__ __forceinline__ void wave_sync_global() {
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 // Collision operator of the layer (build_collision_operators, one pair per lane):
-// K[s][f] = down + electrons, K[f][s] = up + electrons (LDS, stride ldk); the
+// K[s][f] = down + electrons, K[f][s] = up + electrons (LDS, stride ldk = NM | 1); the
 // boundary matrix B (neutrals + A/2, global, stride N) when B != nullptr.
 __device__ __forceinline__ void wave_collisions(const LvgDevProblem &P, const WaveShared &sh, const WaveLayer &sm,
                                                 double *K, int ldk, double *B) {
@@ -665,10 +665,10 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
                     int lc[8];
 #pragma unroll
                     for (int u = 0; u < 8; u++) {
+                        // rows N..NM-1 exist (allocated, unused): fixed offsets, no clamp on N
                         const int r = r0 + u;
-                        const int rr = (r < N) ? r : 0;
-                        kc[u] = K[rr * ldk + d];
-                        const int lv = li[rr * ldk + d];
+                        kc[u] = K[r * ldk + d];
+                        const int lv = li[r * ldk + d];
                         lc[u] = (il && r < N) ? lv : -1;
                     }
 #pragma unroll
@@ -767,12 +767,17 @@ solve_wave_kernel(const LvgDevProblem *__restrict__ Pp, const LvgLaunch *__restr
     __shared__ WaveShared sh;
     const LvgDevProblem &P = *Pp;
     const LvgLaunch &Lc = *Lp;
-    const int N = P.N, ldk = N | 1, wpb = blockDim.x >> 6, w = threadIdx.x >> 6, tid = threadIdx.x;
+    // K / line-index row stride fixed per instantiation: the per-row LDS offsets of the
+    // unrolled row loops (diagonal fold) become instruction immediates instead of address
+    // registers hoisted out of the layer loop (at NM = 48 those spilled, a scratch reload
+    // per LDS read)
+    constexpr int ldk = NM | 1;
+    const int N = P.N, wpb = blockDim.x >> 6, w = threadIdx.x >> 6, tid = threadIdx.x;
     PH_INIT();
     const LvgModeLines &M = Lc.line_overlap ? P.overlap : P.plain;
     int *li = reinterpret_cast<int *>(lvg_wave_dyn);
-    const int li_dbl = (N * ldk + 1) / 2;
-    double *K = lvg_wave_dyn + li_dbl + (int64_t)w * N * ldk;
+    const int li_dbl = (NM * ldk + 1) / 2;
+    double *K = lvg_wave_dyn + li_dbl + (int64_t)w * NM * ldk;
     // block-wide tables: molecule rule, escape/overlap grids, line index map
     for (int e = tid; e < LVG_MAX_CLASSES * LVG_MAX_TERMS; e += blockDim.x) {
         (&sh.ttab[0][0])[e] = (&P.terms.table[0][0])[e];
@@ -825,8 +830,10 @@ solve_wave_kernel(const LvgDevProblem *__restrict__ Pp, const LvgLaunch *__restr
 
 // host-side plan: dynamic LDS bytes of wpb waves for N levels
 inline size_t wave_dyn_bytes(int N, int wpb) {
-    const int ldk = N | 1;
-    return sizeof(double) * ((size_t)(N * ldk + 1) / 2 + (size_t)wpb * N * ldk);
+    // solve_wave_kernel<NM>'s layout: NM rows of stride NM | 1 for the line-index map and
+    // for each wave's K
+    const int nm = N <= 16 ? 16 : ((N + 7) / 8) * 8, ldk = nm | 1;
+    return sizeof(double) * ((size_t)(nm * ldk + 1) / 2 + (size_t)wpb * nm * ldk);
 }
 
 }  // namespace lvg
