@@ -508,33 +508,55 @@ __device__ __forceinline__ Slot make_slot(const LvgDevProblem &P, const LvgLaunc
 // oracle_lu_solve does (iteration_control.h:176): hist_acc[0..np*np) = A, [np*np..) = b;
 // the solution goes to hist_acc[16 + i], its sum to hist_acc[31]
 __device__ __forceinline__ void accel_solve_small(double *hist_acc, int np) {
+    // registers with compile-time indices only (np <= 4): no stack array, no scratch; the
+    // row swap is a select over the candidate rows, the arithmetic that of the loops over np
     double Am[4][4], bv[4];
-    for (int i = 0; i < np; i++) {
-        for (int j = 0; j < np; j++) Am[i][j] = hist_acc[i * np + j];
-        bv[i] = hist_acc[np * np + i];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) Am[i][j] = (i < np && j < np) ? hist_acc[i * np + j] : 0.;
+        bv[i] = (i < np) ? hist_acc[np * np + i] : 0.;
     }
-    for (int k = 0; k < np; k++) {
-        int p = k;
-        double amax = fabs(Am[k][k]);
-        for (int i = k + 1; i < np; i++) if (fabs(Am[i][k]) > amax) { amax = fabs(Am[i][k]); p = i; }
-        if (p != k) {
-            for (int j = 0; j < np; j++) { double x = Am[k][j]; Am[k][j] = Am[p][j]; Am[p][j] = x; }
-            double x = bv[k]; bv[k] = bv[p]; bv[p] = x;
-        }
-        double piv = Am[k][k];
-        for (int i = k + 1; i < np; i++) {
-            double l = Am[i][k] / piv;
-            Am[i][k] = l;
-            for (int j = k + 1; j < np; j++) Am[i][j] = fma(-l, Am[k][j], Am[i][j]);
-            bv[i] = fma(-l, bv[k], bv[i]);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        if (k < np) {
+            int p = k;
+            double amax = fabs(Am[k][k]);
+#pragma unroll
+            for (int i = k + 1; i < 4; i++)
+                if (i < np && fabs(Am[i][k]) > amax) { amax = fabs(Am[i][k]); p = i; }
+#pragma unroll
+            for (int i = k + 1; i < 4; i++) {
+                if (i == p) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) { double x = Am[k][j]; Am[k][j] = Am[i][j]; Am[i][j] = x; }
+                    double x = bv[k]; bv[k] = bv[i]; bv[i] = x;
+                }
+            }
+            double piv = Am[k][k];
+#pragma unroll
+            for (int i = k + 1; i < 4; i++) {
+                if (i < np) {
+                    double l = Am[i][k] / piv;
+                    Am[i][k] = l;
+#pragma unroll
+                    for (int j = k + 1; j < 4; j++) if (j < np) Am[i][j] = fma(-l, Am[k][j], Am[i][j]);
+                    bv[i] = fma(-l, bv[k], bv[i]);
+                }
+            }
         }
     }
-    for (int k = np - 1; k >= 0; k--) {
-        bv[k] /= Am[k][k];
-        double x = bv[k];
-        for (int i = 0; i < k; i++) bv[i] = fma(-Am[i][k], x, bv[i]);
+#pragma unroll
+    for (int k = 3; k >= 0; k--) {
+        if (k < np) {
+            bv[k] /= Am[k][k];
+            double x = bv[k];
+#pragma unroll
+            for (int i = 0; i < k; i++) bv[i] = fma(-Am[i][k], x, bv[i]);
+        }
     }
     double sum = 0.;
-    for (int i = 0; i < np; i++) { sum = sum + bv[i]; hist_acc[16 + i] = bv[i]; }
+#pragma unroll
+    for (int i = 0; i < 4; i++) if (i < np) { sum = sum + bv[i]; hist_acc[16 + i] = bv[i]; }
     hist_acc[31] = sum;
 }
