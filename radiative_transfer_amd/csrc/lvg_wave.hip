@@ -673,18 +673,32 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
                     }
 #pragma unroll
                     for (int u = 0; u < 8; u++) yc[u] = sm.y[lc[u] >= 0 ? lc[u] : 0];
+                    // the skipped terms become subtractions of +0, which leave dg unchanged
+                    // bit for bit, so the dependent chain is the subtractions alone
 #pragma unroll
                     for (int u = 0; u < 8; u++) {
                         const int r = r0 + u;
-                        if (r < N) {
-                            double x = dg - kc[u];
-                            x = (lc[u] >= 0) ? x - yc[u] : x;
-                            dg = (r != d) ? x : dg;
-                        }
+                        const bool on = r < N && r != d;
+                        const double t1 = on ? kc[u] : 0.;
+                        const double t2 = (on && lc[u] >= 0) ? yc[u] : 0.;
+                        dg = dg - t1;
+                        dg = dg - t2;
                     }
                 }
-                if (!M.diag_interleaved)
-                    for (int q = M.diag_ptr[d]; q < M.diag_ptr[d + 1]; q++) dg = dg - sm.y[M.diag_ent[q]];
+                if (!M.diag_interleaved) {
+                    // the line terms of level d in line order, entries and y read 8 at a time
+                    const int q0 = M.diag_ptr[d], q1 = M.diag_ptr[d + 1];
+                    for (int qb = q0; qb < q1; qb += 8) {
+                        int e[8];
+                        double ye[8];
+#pragma unroll
+                        for (int u = 0; u < 8; u++) e[u] = (qb + u < q1) ? M.diag_ent[qb + u] : -1;
+#pragma unroll
+                        for (int u = 0; u < 8; u++) ye[u] = sm.y[e[u] >= 0 ? e[u] : 0];
+#pragma unroll
+                        for (int u = 0; u < 8; u++) dg = dg - ((e[u] >= 0) ? ye[u] : 0.);
+                    }
+                }
             }
             // row `row` of A = K + line terms, diagonal, row 0 <- 1; residual e0 - A n
             double s = (t == 0) ? 1. : 0.;
@@ -704,16 +718,15 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
                     const int j = j0 + u;
-                    if (j < N) {
-                        double v = kc[u];
-                        v = (lc[u] >= 0) ? v + yc[u] : v;
-                        v = (j == row) ? dg : v;
-                        v = (row == 0) ? 1. : v;
-                        a[j] = v;
-                        s = s - v * pc[u];
-                    } else {
-                        a[j] = 0.;
-                    }
+                    double v = kc[u];
+                    v = (lc[u] >= 0) ? v + yc[u] : v;
+                    v = (j == row) ? dg : v;
+                    v = (row == 0) ? 1. : v;
+                    a[j] = (j < N) ? v : 0.;
+                    // columns past N subtract +0 (dg unchanged bit for bit): only the
+                    // subtractions are on the residual's dependent chain
+                    const double pv = v * pc[u];
+                    s = s - ((j < N) ? pv : 0.);
                 }
             }
             eq = wave_max(t < N ? fabs(s) : 0.);
