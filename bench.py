@@ -1,10 +1,14 @@
 #!/usr/bin/env python3
 """Benchmark: layer-iterations/s of the LVG level-population solve (BASELINE.json metric).
 
-Default workload: CH3OH-A, 256 levels, 4096 layers per GPU (BASELINE.json configs[2]),
-layer-sharded over the ranks with dist.shard_range — weak scaling: with `--gpus N` the
-cloud has 4096·N layers (synth_v1) and every rank solves its contiguous block of 4096;
-`--strong` splits one 4096-layer cloud N ways instead. `--workload` selects the other
+Default workload: CH3OH-A, 256 levels, ONE cloud of 4096 layers (BASELINE.json configs[2],
+synth_v1) layer-sharded over the ranks with dist.shard_range — strong scaling, the metric's
+"× 4096 layers, 1/2/4/8 GPU": with `--gpus N` every rank solves its contiguous block of
+about 4096/N layers of the same cloud (the reference's serial layer loop,
+radiative_transfer.cpp:236-256, split N ways). `--weak` gives every rank 4096 layers of a
+4096·N-layer cloud instead (a diagnostic; BASELINE names no such config). The line reports
+`layers_total` (4096 at every N), each rank's share (`shares`: layers, iterations, slowest
+layer, kernel ms) and `max_share_ms`, the slowest rank's kernel time per step. `--workload` selects the other
 BASELINE configs for their own lines: ph2o45_1024 (configs[1]), ch3ohe256_sweep
 (configs[3], 128x128 = 16384 cells), oh24_overlap_2048 (configs[4]). `--chain-len C`
 switches to the reference's default start rule (LVG_INIT_WARM_CHAIN,
@@ -238,7 +242,12 @@ def visible_gpus() -> int:
 
 
 def launch_ranks(args, argv) -> int:
-    """One child per rank, each `bench.py <same args>` with the torch.distributed env."""
+    """One child per rank, each `bench.py <same args>` with the torch.distributed env.
+    The children are killed when one of them fails (the others would wait at a barrier),
+    when the launcher gets SIGINT/SIGTERM, and when `--launch-timeout` seconds pass (a rank
+    hung at a rendezvous or a collective): the launcher then exits non-zero (124 on the
+    deadline) and never leaves ranks holding GPUs behind."""
+    import signal
     n = args.gpus
     if not args.stub:
         have = visible_gpus()
@@ -247,24 +256,49 @@ def launch_ranks(args, argv) -> int:
             return 2
     port = _free_port()
     procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
-    rc = 0
-    live = list(procs)
-    while live:
-        time.sleep(0.2)
-        for p in list(live):
-            c = p.poll()
-            if c is None:
-                continue
-            live.remove(p)
-            if c != 0 and rc == 0:
-                rc = c
-                for q in live:          # a rank failed: the others would wait at a barrier
-                    q.kill()
-    return rc if rc >= 0 else 128 - rc
+
+    def kill_all():
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+        for q in procs:
+            try:
+                q.wait(timeout=30)
+            except Exception:
+                pass
+
+    def on_signal(signum, _frame):
+        kill_all()
+        sys.exit(128 + signum)
+
+    old = {sig: signal.signal(sig, on_signal) for sig in (signal.SIGINT, signal.SIGTERM)}
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+        rc = 0
+        live = list(procs)
+        deadline = time.monotonic() + args.launch_timeout
+        while live:
+            time.sleep(0.2)
+            if time.monotonic() > deadline:
+                print(f"bench.py: ranks still running after {args.launch_timeout:.0f} s; killed", file=sys.stderr)
+                kill_all()
+                return 124
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c
+                    kill_all()          # a rank failed: the others would wait at a barrier
+                    live = []
+        return rc if rc >= 0 else 128 - rc
+    finally:
+        for sig, h in old.items():
+            signal.signal(sig, h)
 
 
 # ---- one rank -----------------------------------------------------------------------------
@@ -290,7 +324,7 @@ class StubSolver:
         return 0.0
 
     def last_kernel_kind(self):
-        return 0
+        return 0 if self.N else -1
 
     def close(self):
         pass
@@ -325,7 +359,7 @@ def run_rank(args) -> int:
     kind, N, L_cfg, seed = synth.CONFIGS[args.workload]
     N = args.nb_lev or N
     L_cloud = args.layers or L_cfg
-    total = L_cloud if args.strong else L_cloud * world
+    total = L_cloud * world if args.weak else L_cloud
     prob, layers_all, o = synth.make_problem(args.workload, nb_lay=total, nb_lev=N)
     opts = abi.default_opts(**o)
     if args.chain_len:
@@ -391,16 +425,22 @@ def run_rank(args) -> int:
         td.barrier()
     elapsed = time.perf_counter() - t0
     prov_rec = prov.timed_end()
-    kernel_kind = solver.last_kernel_kind() if n_mine > 0 else 0
+    # the kernel the ABI chose; -1 (none) on a rank with no layers (the ABI reports -1 for
+    # an empty launch too)
+    kernel_kind = solver.last_kernel_kind() if n_mine > 0 else -1
     st2 = dist.status_numpy(status[:n_mine])
     assert int(st2["iterations"].sum()) == units_local, "iteration count changed between steps"
+    # this rank's share: [lo, hi), iterations, slowest layer, mean kernel ms, step ms
+    mine_rec = [float(lo), float(hi), float(units_local), float(max_layer_its),
+                float(np.mean(kern_ms)) if n_mine else 0.0, 1e3 * elapsed / args.steps, float(kernel_kind)]
+    shares = [mine_rec]
     if multi:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        td.all_reduce(tt, op=td.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        ml = torch.tensor([float(max_layer_its)], dtype=torch.float64, device=dev)
-        td.all_reduce(ml, op=td.ReduceOp.MAX)
-        max_layer_its = int(ml.item())
+        rec = torch.tensor(mine_rec, dtype=torch.float64, device=dev)
+        outs = [torch.zeros_like(rec) for _ in range(world)]
+        td.all_gather(outs, rec)
+        shares = [o.cpu().tolist() for o in outs]
+        elapsed = max(r[5] for r in shares) * args.steps / 1e3          # max over ranks
+        max_layer_its = int(max(r[3] for r in shares))
     units_total, nonconv, max_rel = int(glob[0].item()), int(glob[1].item()), float(glob[2].item())
 
     host_value = None
@@ -415,23 +455,27 @@ def run_rank(args) -> int:
     if rank == 0:
         print(json.dumps(report(args, world, N, total, L_cfg, lo, hi, units_total, units_local, nonconv, max_rel,
                                 max_layer_its, elapsed, kern_ms, coll_ms, opts, offs, prov_rec, host_value,
-                                prob, mine, stub, kernel_kind)), flush=True)
+                                prob, mine, stub, kernel_kind, shares)), flush=True)
     solver.close()
     if multi:
         td.destroy_process_group()
     return 0
 
 
+KERNELS = {-1: "none (empty launch)", 0: "lvg::solve_kernel", 1: "lvg::solve_wave_kernel",
+           2: "lvg_wide::solve_kernel", 3: "lvg_big::solve_kernel"}
+
+
 def report(args, world, N, total, L_cfg, lo, hi, units_total, units_local, nonconv, max_rel, max_layer_its,
-           elapsed, kern_ms, coll_ms, opts, offs, prov_rec, host_value, prob, mine, stub, kernel_kind=0):
+           elapsed, kern_ms, coll_ms, opts, offs, prov_rec, host_value, prob, mine, stub, kernel_kind=0,
+           shares=None):
     from radiative_transfer_amd import synth
     value = units_total * args.steps / elapsed
     kms = float(np.mean(kern_ms))
     cms = float(np.mean(coll_ms))
     ms_step = 1e3 * elapsed / args.steps
     # the kernel the ABI chose for this launch (lvg_last_kernel_kind)
-    kernel = {0: "lvg::solve_kernel", 1: "lvg::solve_wave_kernel", 2: "lvg_wide::solve_kernel",
-              3: "lvg_big::solve_kernel"}[kernel_kind]
+    kernel = KERNELS[kernel_kind]
     bound = binding_roof(N)
     per_launch = units_local
     F, B = flops_per_layer_iteration(N), bytes_per_layer_iteration(N)
@@ -473,13 +517,13 @@ def report(args, world, N, total, L_cfg, lo, hi, units_total, units_local, nonco
     out = {
         "metric": METRIC, "value": value, "unit": UNIT, "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
-        "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "f64",
+        "scaling": "weak" if args.weak else "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (synth_v1, SURVEY.md 8d)" + (" [STUB solver: launcher test]" if stub else ""),
         # a level or layer count other than the config's is named in the workload label
         "config": {"workload": args.workload + (f"_nblev{N}" if N != synth.CONFIGS[args.workload][1] else "")
                    + (f"_layers{args.layers}" if args.layers and args.layers != L_cfg else ""),
                    "nb_lev": N, "layers_total": total,
-                   "layers_per_gpu": layers_rank if world == 1 or not args.strong
+                   "layers_per_gpu": layers_rank if world == 1 or args.weak
                    else f"{total // world}-{-(-total // world)}",
                    "layer_iterations_per_step": units_total, "nonconverged_layers": nonconv,
                    "max_rel_error": max_rel,
@@ -489,6 +533,12 @@ def report(args, world, N, total, L_cfg, lo, hi, units_total, units_local, nonco
                    else "boundary_layer", "acceleration": bool(opts.acceleration),
                    "line_overlap": bool(opts.line_overlap), "tuning": args.tuning or None},
         "roofline": roof,
+        # per rank: its layer block [lo, hi), layer-iterations, slowest layer's iterations,
+        # mean kernel ms and timed ms per step, the kernel it ran; the step is the slowest share
+        "shares": [{"rank": r, "lo": int(s[0]), "hi": int(s[1]), "layers": int(s[1] - s[0]),
+                    "iterations": int(s[2]), "max_layer_iterations": int(s[3]), "kernel_ms": s[4],
+                    "ms_per_step": s[5], "kernel": KERNELS[int(s[6])]} for r, s in enumerate(shares or [])],
+        "max_share_ms": max((s[4] for s in shares), default=kms) if shares else kms,
         "provenance": prov_rec,
     }
     if host_value is not None:
@@ -505,9 +555,13 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="ch3oha256_4096")
-    ap.add_argument("--layers", type=int, default=0, help="layers per GPU (--strong: of the cloud); default the config's")
+    ap.add_argument("--layers", type=int, default=0, help="layers of the cloud (--weak: per GPU); default the config's")
     ap.add_argument("--nb-lev", type=int, default=0, help="levels (default: the config's; 768 = reference CH3OH)")
-    ap.add_argument("--strong", action="store_true", help="split ONE cloud of the config's layers over the GPUs")
+    ap.add_argument("--strong", action="store_true",
+                    help="split ONE cloud of the config's layers over the GPUs (the default; kept for old command lines)")
+    ap.add_argument("--weak", action="store_true", help="every GPU solves the config's layers (a cloud N times larger)")
+    ap.add_argument("--launch-timeout", type=float, default=3000.0,
+                    help="seconds before the launcher kills ranks that have not finished")
     ap.add_argument("--chain-len", type=int, default=0,
                     help="warm chains of this many layers (LVG_INIT_WARM_CHAIN) instead of independent layers")
     ap.add_argument("--tuning", default="", help="lvg_set_tuning spec (diagnostics; results unchanged)")
@@ -517,6 +571,8 @@ def main(argv=None):
     ap.add_argument("--no-provenance", action="store_true")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)   # launcher test, CPU only
     args = ap.parse_args(argv)
+    if args.weak and args.strong:
+        ap.error("--weak and --strong exclude each other")
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
         return launch_ranks(args, argv)
     return run_rank(args)

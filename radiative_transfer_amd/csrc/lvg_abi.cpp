@@ -69,8 +69,11 @@ struct ModeHost {
 }  // namespace
 
 // Tuning and diagnostics (not results: every setting gives bit-identical populations and
-// status). Defaults, then the LVG_TUNING environment variable once at lvg_create, then
-// lvg_set_tuning; the format is "key=value,key=value" with the keys below.
+// status). Defaults, then the LVG_TUNING environment variable once at lvg_create (a spec
+// that does not parse is ignored with a message on stderr: it never stops a handle from
+// being created), then lvg_set_tuning, whose keys are MERGED into the current settings
+// (keys it does not name keep their value; an empty spec resets to the defaults). The
+// format is "key=value,key=value" with the keys below.
 struct LvgTuning {
     int block_kernel = 0;      // block_kernel=1: the block kernel also for N <= 64
     int queue_order = 1;       // queue_order=0: work queue in layer order, not longest-expected-first
@@ -99,7 +102,8 @@ struct lvg_handle {
     int64_t ws_stride = 0;
     int *counter = nullptr;
     size_t lds_cap = 0;            // LDS bytes per workgroup (wave kernel plan)
-    int last_kernel = 0;           // lvg_last_kernel_kind: 0 block, 1 wave, 2 512-thread, 3 768-thread kernel
+    int last_kernel = -1;          // lvg_last_kernel_kind: -1 none (no launch yet, or an empty batch),
+                                   // 0 block, 1 wave, 2 512-thread, 3 768-thread kernel
     // scratch for host-buffer solves
     double *d_soa = nullptr, *d_pops = nullptr;
     void *d_status = nullptr;
@@ -718,7 +722,8 @@ int lvg_abi_version(void) { return LVG_ABI_VERSION; }
 
 int lvg_set_tuning(lvg_handle *h, const char *spec) {
     if (!h) return LVG_E_STATE;
-    LvgTuning t;
+    // merged into the current settings (the environment's included); "" resets them
+    LvgTuning t = (spec && *spec) ? h->tune : LvgTuning();
     const int rc = parse_tuning(h, spec, t);
     if (rc == LVG_OK) h->tune = t;
     return rc;
@@ -776,7 +781,13 @@ int lvg_create(const lvg_problem *prob, int device, lvg_handle **out) {
     lvg_handle *h = new (std::nothrow) lvg_handle();
     if (!h) return fail(nullptr, LVG_E_NOMEM, "out of host memory");
     int rc = validate(h, prob);
-    if (rc == LVG_OK) rc = parse_tuning(h, std::getenv("LVG_TUNING"), h->tune);
+    if (rc == LVG_OK) {
+        // diagnostics only: a bad LVG_TUNING is reported and ignored, never fatal
+        LvgTuning t;
+        if (parse_tuning(h, std::getenv("LVG_TUNING"), t) == LVG_OK) h->tune = t;
+        else std::fprintf(stderr, "liblvg_amd: LVG_TUNING ignored (%s)\n", h->err.c_str());
+        h->err.clear();
+    }
     if (rc == LVG_OK) {
         h->device = device;
         hipError_t e = hipSetDevice(device);
@@ -839,6 +850,7 @@ int launch_solve(lvg_handle *h, int nb_lay, const double *d_soa, double *d_pops,
     int rc;
     h->last_ms = 0.;
     h->last_launches = 0;
+    h->last_kernel = -1;            // an empty batch launches nothing
     if (nb_lay == 0) return LVG_OK;
     HIPCHECK(h, hipSetDevice(h->device));
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;

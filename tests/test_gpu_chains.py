@@ -28,21 +28,26 @@ def _cmp_chains(s, P, L, off, opts):
     return po, so
 
 
-@pytest.mark.parametrize("name,nl,force_block", [("ph2o45_1024", 40, False), ("ph2o45_1024", 14, True),
-                                                 ("oh24_overlap_2048", 24, False), ("ch3oha256_4096", 9, False)])
-def test_chains_bit_exact(name, nl, force_block):
+# kind: the kernel the chains must run on (1 wave, 0 the 256-thread and 2 the 512-thread
+# block kernel; the last two pinned with wide=0 / wide=2)
+@pytest.mark.parametrize("name,nl,kind", [("ph2o45_1024", 40, 1), ("ph2o45_1024", 14, 0), ("ph2o45_1024", 14, 2),
+                                          ("oh24_overlap_2048", 24, 1), ("ch3oha256_4096", 9, 0),
+                                          ("ch3oha256_4096", 9, 2)])
+def test_chains_bit_exact(name, nl, kind):
     P, L, o = synth.make_problem(name, nb_lay=nl)
     s = LvgSolver(P)
     # ragged chains, an empty one, a single-layer one
     cuts = sorted({0, nl, 1, nl // 3, nl // 3, (2 * nl) // 3})
     off = np.array(cuts + ([nl] if cuts[-1] != nl else []), dtype=np.int32)
     off = np.concatenate([off[:2], off[1:2], off[2:]])            # duplicate offset: empty chain
-    s.set_tuning("block_kernel=1" if force_block else "")
+    s.set_tuning("" if kind == 1 else f"block_kernel=1,wide={kind}")
     po, so = _cmp_chains(s, P, L, off, abi.default_opts(init=WARM, **o))
+    assert s.last_kernel_kind() == kind
     # caps that leave layers unconverged mid-chain: the next layer restarts from the
     # boundary populations (the is_solution_found_prev branch)
     kw = {"max_iter_acc": 3, "allow_plain_retry": 0} if o.get("acceleration", 1) else {"max_iter_plain": 3}
     po, so = _cmp_chains(s, P, L, off, abi.default_opts(init=WARM, **{**o, **kw}))
+    assert s.last_kernel_kind() == kind
     assert (so["converged"] == 0).any() and (so["converged"] == 1).any()
     s.close()
 

@@ -27,6 +27,16 @@ from parity_helpers import assert_same, overlap_dx
 
 pytestmark = pytest.mark.gpu
 
+# The block kernel comes in two instantiations for N <= 256 (lvg_kernels.hip): the
+# 256-thread one (kind 0, launches that fill the chip) and the 512-thread one (kind 2,
+# picked automatically for launches of at most two layers per CU — every small test
+# here). `wide=0` / `wide=2` pin each one; the tests assert the kind that ran.
+BLOCK_KINDS = [pytest.param(0, id="bt256"), pytest.param(2, id="bt512")]
+
+
+def _block_tuning(kind, *extra):
+    return ",".join(("block_kernel=1", f"wide={kind}") + extra)
+
 
 def _cmp(s, P, L, opts, pops=None, equal_nan=False):
     pg, sg = s.solve_layers(L, opts, pops=pops)
@@ -35,11 +45,12 @@ def _cmp(s, P, L, opts, pops=None, equal_nan=False):
     return po, so
 
 
-@pytest.mark.parametrize("name,nl,force_block", [("ch3oha256_4096", 6, False), ("ph2o45_1024", 12, True)])
-def test_block_kernel_option_paths(name, nl, force_block):
+@pytest.mark.parametrize("kind", BLOCK_KINDS)
+@pytest.mark.parametrize("name,nl", [("ch3oha256_4096", 6), ("ph2o45_1024", 12)])
+def test_block_kernel_option_paths(name, nl, kind):
     P, L, o = synth.make_problem(name, nb_lay=nl)
     s = LvgSolver(P)
-    s.set_tuning("block_kernel=1" if force_block else "")
+    s.set_tuning(_block_tuning(kind))
     variants = [{"accel_start": 2, "accel_nb": 2, "accel_period": 1},                 # Ng from iteration 2
                 {"accel_start": 3, "accel_nb": 3, "accel_period": 2, "max_iter_acc": 9},
                 {"max_iter_acc": 2, "allow_plain_retry": 0},                          # cap -> best iterate
@@ -49,6 +60,7 @@ def test_block_kernel_option_paths(name, nl, force_block):
     for kw in variants:
         opts = abi.default_opts(**{**o, **kw})
         po, so = _cmp(s, P, L, opts)
+        assert s.last_kernel_kind() == kind
         if opts.acceleration and (so["iterations"] > opts.accel_start).any():
             ran_accel = True
     assert ran_accel, "no layer reached the Ng step"
@@ -57,7 +69,9 @@ def test_block_kernel_option_paths(name, nl, force_block):
     p0, _ = oracle.solve_layers(P, L, base)
     guess = 0.5 * p0 + 0.5 / P.mol.nb_lev
     _cmp(s, P, L, abi.default_opts(init=abi.LVG_INIT_GIVEN, **o), pops=guess)
+    assert s.last_kernel_kind() == kind
     _cmp(s, P, L, abi.default_opts(init=abi.LVG_INIT_WARM_CHAIN, **o))
+    assert s.last_kernel_kind() == kind
     s.close()
 
 
@@ -108,12 +122,13 @@ def _generic_problem():
 
 
 @pytest.mark.parametrize("make", [_oh_nonhf_problem, _generic_problem], ids=["oh_nonhf_q10", "generic_q5"])
-@pytest.mark.parametrize("force_block", [False, True], ids=["auto", "block"])
-def test_collision_rules(make, force_block):
+@pytest.mark.parametrize("kind", [pytest.param(1, id="wave")] + BLOCK_KINDS)
+def test_collision_rules(make, kind):
     P, L, o = make()
     s = LvgSolver(P)
-    s.set_tuning("block_kernel=1" if force_block else "")
+    s.set_tuning("" if kind == 1 else _block_tuning(kind))
     _cmp(s, P, L, abi.default_opts(**o))
+    assert s.last_kernel_kind() == kind
     bo = oracle.boundary_layer_populations(P, L)
     Mg, dfg, pg, eg = s.debug_calc_new_pop(L, 0, bo[0], 0)
     Mo, dfo, po, eo = oracle.calc_new_pop(P, L, 0, bo[0], 0)
@@ -182,9 +197,10 @@ def test_async_device_solve_then_host_entry_on_same_handle():
     s.close()
 
 
+@pytest.mark.parametrize("kind", BLOCK_KINDS)
 @pytest.mark.parametrize("make", [lambda: synth.make_problem("ch3oha256_4096", nb_lay=12), _generic_problem],
                          ids=["ch3oha256", "generic_electrons"])
-def test_collision_build_paths(make):
+def test_collision_build_paths(make, kind):
     """Independent layers on the block kernel with the collision operators built in the
     solve kernel (the default), built ahead by coll_kernel (B formed from K without
     electron tables, B stored with them), and with coll_kernel asked for but over its
@@ -194,13 +210,15 @@ def test_collision_build_paths(make):
     s = LvgSolver(P)
     opts = abi.default_opts(**o)
     po, so = oracle.solve_layers(P, L, opts)
-    for spec, ahead in (("block_kernel=1", False), ("block_kernel=1,coll_ahead=1", True),
-                        ("block_kernel=1,coll_ahead=1,coll_order=0", True),
-                        ("block_kernel=1,coll_ahead=1,coll_mem=0", False)):
+    for extra, ahead in (((), False), (("coll_ahead=1",), True), (("coll_ahead=1", "coll_order=0"), True),
+                         (("coll_ahead=1", "coll_mem=0"), False)):
+        spec = _block_tuning(kind, *extra)
+        s.set_tuning("")                         # set_tuning merges: start from the defaults
         s.set_tuning(spec)
         pg, sg = s.solve_layers(L, opts)
         assert_same(pg, sg, po, so)
         assert (s.last_coll_time() > 0) == ahead, spec
+        assert s.last_kernel_kind() == kind, spec
     with pytest.raises(Exception):
         s.set_tuning("no_such_key=1")
     s.close()
