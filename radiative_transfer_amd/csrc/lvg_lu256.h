@@ -453,7 +453,9 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             if (w > wq && nw > 0) lu2_apply(acc, prow, false, kk, nb, SLO, cw0, nw, A, N, sm);
         }
     }
+    TSTAMP(tw0);
     __syncthreads();
+    TACC(PH_BS_WAIT, tw0);
     back_substitute(A, N, b, sm);
     double emax = 0.;
     if (FUSED && t < N) { const double r = sm.resid[t]; src.df[t] = r; emax = fabs(r); }

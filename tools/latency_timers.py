@@ -41,4 +41,7 @@ it = int(ss["iterations"][0])
 print(f"{name}: layer {k} alone, {it} iterations, kernel {ms:.3f} ms = {ms * 1e-3 * 2.3e9 / it:.0f} cyc/iteration at 2.3 GHz")
 for i, n in enumerate(names):
     print(f"  {n:16s} {cyc[i] / it:10.0f} cyc/iteration")
+for i, n in [(15, "  (residual hand-off)"), (12, "  (block load)"), (16, "  (L fetch+stage)"), (17, "  (TRSM)"),
+             (21, "  (pre-panel bar+dump)"), (22, "  (bsub diag)"), (23, "  (bsub update)"), (24, "  (wait before bsub)")]:
+    print(f"  {n:22s} {cyc[i] / it:10.0f} cyc/iteration")
 print(f"  sum of phases    {cyc[:9].sum() / it:10.0f} cyc/iteration; raw slots {buf[:32]}")
