@@ -91,39 +91,6 @@ __device__ __forceinline__ double readlane_d(double x, int lane) {
     return __hiloint2double(hi, lo);
 }
 
-// ------------------------------------------------------------------------------
-// fp64 division split in two (the pivot divisions of the LUs and their back substitutions)
-// ------------------------------------------------------------------------------
-// hipcc lowers x / y on gfx950 to v_div_scale(y), v_rcp_f64, two Newton steps
-// (v_fma, v_fmac) giving r, v_div_scale(x), q0 = x * r, e = fma(-y, q0, x),
-// v_div_fmas(e, r, q0), v_div_fixup. When both operands lie in [2^-300, 2^301) in
-// magnitude, v_div_scale rescales neither (exponent difference < 768, no denormal
-// operand, reciprocal or quotient, numerator exponent > 53), v_div_fmas is a plain fma
-// and v_div_fixup returns the value with the sign it already has, so
-//     x / y == ldiv(x, y, ldiv_rcp(y))   bit for bit,
-// with r = ldiv_rcp(y) depending on y alone. A pivot's r is computed once (or ahead,
-// off the dependent chain), which leaves three dependent operations per quotient on the
-// chain instead of eleven. x == 0 gives x * y (the signed zero v_div_fixup returns);
-// any other operand outside the range takes the plain division.
-__device__ __forceinline__ double ldiv_rcp(double y) {
-    const double r0 = __builtin_amdgcn_rcp(y);
-    const double r1 = fma(r0, fma(-y, r0, 1.), r0);
-    return fma(r1, fma(-y, r1, 1.), r1);
-}
-__device__ __forceinline__ bool ldiv_range(double v) {
-    return ((((unsigned)__double2hiint(v)) >> 20) & 0x7ffu) - 723u <= 600u;
-}
-__device__ __forceinline__ double ldiv(double x, double y, double r) {
-#ifdef LVG_NO_LDIV                              // diagnostic A/B build: the plain division
-    return x / y;
-#endif
-    if (ldiv_range(y) && (x == 0. || ldiv_range(x))) {
-        const double q0 = x * r;
-        return x == 0. ? x * y : fma(fma(-y, q0, x), r, q0);
-    }
-    return x / y;
-}
-
 // Pivot key of oracle_lu_solve's rule (largest |v|, first maximum wins; amax seeded with
 // |a_kk| and replaced on a strict '>', so a NaN below never wins and a NaN on the
 // diagonal always does): |v| >= 0 orders like its bit pattern; rows still taking part

@@ -278,18 +278,13 @@ __device__ __forceinline__ void back_substitute(const double *A, int N, const do
         if (t < 64) {
             // diagonal block by wave 0 in registers: lane r < nb holds b_r and row r of the
             // block; x_m (lane m's b_m / U_mm once final) is broadcast by DPP row_newbcast:m
-            // x_m = b_m / U_mm as ldiv with the reciprocal part of each U_mm formed ahead
-            // (lane m: its diagonal and reciprocal, read by the step through DPP), so
-            // the chain of a step is b_m's broadcast, three operations and the update
             const int r = t & 15;
             double bt = (t < nb) ? sm.blog[k0 + t] : 0., ur[NB];
 #pragma unroll
             for (int m = 0; m < NB; m++) ur[m] = (t < nb) ? sm.L11[r][m] : 1.;
-            const double dr = (t < nb) ? sm.L11[r][r] : 1., rr = ldiv_rcp(dr);
 #define LVG_BSUB_STEP(M_)                                                                  \
             if ((M_) < nb) {                                                               \
-                const double xm = ldiv(dpp_d<0x150 + (M_), 0xf, 0xf>(bt), dpp_d<0x150 + (M_), 0xf, 0xf>(dr), \
-                                       dpp_d<0x150 + (M_), 0xf, 0xf>(rr));                 \
+                const double xm = dpp_d<0x150 + (M_), 0xf, 0xf>(bt / ur[M_]);              \
                 if (r < (M_)) bt = fma(-ur[M_], xm, bt);                                   \
                 else if (r == (M_)) bt = xm;                                               \
             }

@@ -408,9 +408,6 @@ __device__ __forceinline__ void wave_lu_solve(double (&a)[NM], double rb, int N,
     unsigned khi, klo, H;
     pivot_key(a[0], act, lp == 0, khi, klo);
     H = wave_max_u32(khi);
-    // the reciprocal part of the pivot division (ldiv), ahead for every candidate row:
-    // it overlaps the max-key reduction, and the pivot lane's is read with the pivot
-    double rsp = ldiv_rcp(a[0]);
 #pragma unroll
     for (int c = 0; c < NM; c++) {
         if (c < N) {
@@ -427,17 +424,15 @@ __device__ __forceinline__ void wave_lu_solve(double (&a)[NM], double rb, int N,
             pl = __builtin_amdgcn_readfirstlane(pl);
             const int plp = __builtin_amdgcn_readlane(lp, pl);
             const double piv = readlane_d(a[c], pl);
-            const double rpv = readlane_d(rsp, pl);
             const double bc = readlane_d(rb, pl);
             if (ln == pl) { act = false; lp = c; }
             else if (lp == c) lp = plp;
-            const double l = ldiv(a[c], piv, rpv);      // == a[c] / piv
+            const double l = a[c] / piv;
             if (c + 1 < NM) {
                 const double u = readlane_d(a[c + 1], pl);
                 a[c + 1] = act ? fma(-l, u, a[c + 1]) : a[c + 1];
                 pivot_key(a[c + 1], act, lp == c + 1, khi, klo);
                 H = wave_max_u32(khi);
-                rsp = ldiv_rcp(a[c + 1]);
             }
 #pragma unroll
             for (int j = c + 2; j < NM; j++) {
@@ -452,11 +447,8 @@ __device__ __forceinline__ void wave_lu_solve(double (&a)[NM], double rb, int N,
 #pragma unroll
     for (int k = NM - 1; k >= 0; k--) {
         if (k < N) {
-            // x_k = b_k / U_kk on the owner's values, as ldiv: U_kk and its reciprocal
-            // part do not depend on the chain, so only b_k's read and three operations do
             const int ow = __builtin_amdgcn_readfirstlane(__ffsll((long long)__ballot(ln < N && lp == k)) - 1);
-            const double dk = readlane_d(a[k], ow);
-            const double xk = ldiv(readlane_d(rb, ow), dk, ldiv_rcp(dk));
+            const double xk = readlane_d(rb / a[k], ow);
             if (ln == ow) rb = xk;
             else if (lp < k) rb = fma(-a[k], xk, rb);
         }
