@@ -30,7 +30,7 @@ constexpr int S4 = NMAX / 64;   // row slots per lane: tile row 64 s + lane
 constexpr int CW = LU_CW;       // columns per wave = chunk (panel) width: 16 or 8
 constexpr int BW = NW * CW;     // block-column width: 64 (4 waves) or 128 (8 waves, LVG_WIDE)
 constexpr int CL = CW / 4;      // TRSM columns per lane (4 x 16-lane rows)
-static_assert(CW == 16, "chunk width: the TRSM and the panel assume 16 columns per wave");
+static_assert(CW == 16 || CW == 8, "chunk width: the TRSM lays 16 rows over 16-lane groups");
 
 // LDS stores of one lane visible to the other lanes of its wave: a wave's LDS instructions
 // execute in issue order, so only compiler motion has to be stopped (wavefront-scope
@@ -42,6 +42,7 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+#if !LVG_LU3
 // One chunk applied to this wave's columns: the chunk's pivot rows (tile rows kk.. for an
 // earlier chunk, the rows whose logical position is kk.. for one of this block) published
 // by their owner lanes to Ub[w], solved against L11 (x_r takes its updates for m ascending,
@@ -120,6 +121,8 @@ __device__ __forceinline__ void lu2_apply(double (&acc)[S4][CW], const int (&pro
     }
     TACC(PH_GEMM, tg0);
 }
+
+#endif
 
 // The chunk kk (this wave's CW columns) factored by this wave alone: rows of slots >= s_lo
 // whose logical position is >= kk take part (exec-masked), 4 rows per lane. Per column:
@@ -235,6 +238,7 @@ __device__ __forceinline__ void lu2_panel(double (&acc)[S4][CW], const int (&pro
     }
 }
 
+#if !LVG_LU3
 // The factored chunk's rows (logical position >= kk) to A (L below the pivots; the pivot
 // rows with L11 and U), perm/pos/b, L11 (strictly lower) and the
 // stage Lst (L of the rows below the chunk, 0 for the others) for the waves to its right.
@@ -461,3 +465,6 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
     if (FUSED && t < N) { const double r = sm.resid[t]; src.df[t] = r; emax = fabs(r); }
     return FUSED ? block_max(emax, sm) : 0.;
 }
+#else
+#include "lvg_lu3.h"
+#endif

@@ -1,0 +1,348 @@
+// lvg_lu3.h — the N <= 256 LU with the waves pipelined over chunks (LVG_LU3), included by
+// lvg_lu256.h after lu2_panel.
+//
+// lu_matrix_solve (absent library; call sites iteration_lvg.cpp:100, iteration_control.cpp:87)
+// as a left-looking LU over chunks of CW = 16 columns, chunk j owned by wave j mod NW, with
+// no workgroup barrier between chunks:
+//  * A wave takes its next chunk as soon as it has published the previous one: it loads the
+//    chunk's columns (assembled from K, the line terms and the diagonal when fused) for the
+//    tile rows of a consistent snapshot of the row permutation (seqlock on sm.seq: positions
+//    of published chunks are final, so their rows sit at their own tile rows), adds the
+//    chunk's columns to the residual in column order (chunks in turn, sm.rdone), then
+//    applies chunks 0 .. j-1 in order, waiting only for those not yet published, and factors
+//    the chunk (lu2_panel) and publishes it.
+//  * Applying chunk i: the chunk's pivot rows in this wave's columns are solved against
+//    L11 of chunk i (kept in LDS for every chunk) and stored as U rows; the rows below take
+//    the rank-16 update with L read straight from the factors in A (4 columns of L at a
+//    time), U broadcast from the wave's LDS rows.
+//  * Publishing chunk j: L and the pivot rows to A, perm / pos / b, L11 of the chunk, then
+//    sm.seq = 2 (j + 1) behind a workgroup release fence.
+// So while the owner of chunk j factors it, the other waves already apply the published
+// chunks to their next chunks instead of waiting at a barrier; the chain is panel j ->
+// apply of j to chunk j+1 -> panel j+1.
+// Every element still receives fma(-l_ik, u_kj, a_ij) for k ascending and the pivots are
+// those of lu2_panel (the oracle's rule), so the results are the unblocked oracle's bit for
+// bit. On return sm.blog holds x.
+
+#ifndef LVG_LU3_PRIO
+#define LVG_LU3_PRIO 0
+#endif
+__device__ __forceinline__ int lu3_ld(const int &x) {
+    return __hip_atomic_load(&x, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lu3_st(int &x, int v) {
+    __hip_atomic_store(&x, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// the wave waits (sleeping between polls) until the sequence word reaches v
+__device__ __forceinline__ void lu3_wait(const int &x, int v) {
+    while (lu3_ld(x) < v) __builtin_amdgcn_s_sleep(1);
+}
+
+// Chunk ci (columns kk.., nb of them, published) applied to this wave's columns cw0.. (nw).
+// earlier: ci was published before this chunk's load, so its pivot rows sit at tile rows
+// kk..kk+15 and the rows taking its update at tile rows >= kk + 16. s_up: first row slot
+// that can hold a row taking an update (tile rows below 16 x the chunks final at the load
+// are pivots of earlier chunks).
+__device__ __forceinline__ void lu3_apply(double (&acc)[S4][CW], const int (&prow)[S4], bool earlier, int ci, int nb,
+                                          int s_up, int cw0, int nw, double *A, int N, Smem &sm) {
+    const int l = threadIdx.x & 63, w = threadIdx.x >> 6, kk = ci * CW;
+    double (*Ub)[CW] = sm.Ub[w];
+    TSTAMP(ta0);
+    // the chunk's pivot rows in this wave's columns to Ub (their owner lanes)
+#pragma unroll
+    for (int s = 0; s < S4; s++) {
+        const int r = 64 * s + l;
+        if (s >= (earlier ? kk >> 6 : s_up) && r < N) {
+            const int q = (earlier ? r : sm.pos[prow[s]]) - kk;
+            if (q >= 0 && q < nb) {
+                double2 *d = reinterpret_cast<double2 *>(&Ub[q][0]);
+#pragma unroll
+                for (int j = 0; j < CW / 2; j++) d[j] = make_double2(acc[s][2 * j], acc[s][2 * j + 1]);
+            }
+        }
+    }
+    wave_lds_sync();
+    {
+        const int q4 = l >> 4, r = l & 15;        // lane: row r of the chunk, columns CL*q4..
+        double x[CL];
+        if (r < CW) {
+#pragma unroll
+            for (int i = 0; i < CL; i++) x[i] = Ub[r][CL * q4 + i];
+        }
+#if LVG_NARROW
+        // L11 of the chunk from the factors in A (row r of the chunk: its pivot row, whose
+        // values left of its pivot column are L11; the TRSM reads only those)
+        double lrw[CW];
+        {
+            const double *lsrc11 = A + (int64_t)sm.perm[kk + (r < nb ? r : 0)] * N + kk;
+            if ((N & 1) == 0) {
+                const double2 *l2 = reinterpret_cast<const double2 *>(lsrc11);
+#pragma unroll
+                for (int m = 0; m < CW / 2; m++) { const double2 v = l2[m]; lrw[2 * m] = v.x; lrw[2 * m + 1] = v.y; }
+            } else {
+#pragma unroll
+                for (int m = 0; m < CW; m++) lrw[m] = lsrc11[m];
+            }
+        }
+#else
+        const double *lrw = sm.pu.L11c[ci][r < CW ? r : 0];
+#endif
+#define LVG_TRSM_STEP(M_)                                                                  \
+        if ((M_) < nb - 1) {                                                               \
+            const double lm = lrw[M_];                                                     \
+            _Pragma("unroll") for (int i = 0; i < CL; i++) {                               \
+                const double y = dpp_d<0x150 + (M_), 0xf, 0xf>(x[i]);                      \
+                if (r > (M_)) x[i] = fma(-lm, y, x[i]);                                    \
+            }                                                                              \
+        }
+        LVG_TRSM_STEP(0) LVG_TRSM_STEP(1) LVG_TRSM_STEP(2) LVG_TRSM_STEP(3)
+        LVG_TRSM_STEP(4) LVG_TRSM_STEP(5) LVG_TRSM_STEP(6) LVG_TRSM_STEP(7)
+        LVG_TRSM_STEP(8) LVG_TRSM_STEP(9) LVG_TRSM_STEP(10) LVG_TRSM_STEP(11)
+        LVG_TRSM_STEP(12) LVG_TRSM_STEP(13) LVG_TRSM_STEP(14)
+#undef LVG_TRSM_STEP
+        if (r < nb) {
+#pragma unroll
+            for (int i = 0; i < CL; i++) Ub[r][CL * q4 + i] = x[i];
+            double *urow = A + (int64_t)sm.perm[kk + r] * N + cw0 + CL * q4;
+#pragma unroll
+            for (int i = 0; i < CL; i++) if (CL * q4 + i < nw) urow[i] = x[i];
+        }
+    }
+    wave_lds_sync();
+    TACC(PH_T_SOLVE, ta0);
+    TSTAMP(tg0);
+    // rows taking the update: below the chunk's pivots (logical position >= kk + nb)
+    bool take[S4];
+    const double *lsrc[S4];
+#pragma unroll
+    for (int s = 0; s < S4; s++) {
+        const int r = 64 * s + l;
+        take[s] = s >= s_up && r < N && (earlier ? r : sm.pos[prow[s]]) >= kk + nb;
+        lsrc[s] = A + (int64_t)(take[s] ? prow[s] : 0) * N + kk;
+    }
+#ifndef LVG_LU3_MG
+#define LVG_LU3_MG 4
+#endif
+    constexpr int MG = LVG_LU3_MG;                // columns of L per load group
+#pragma unroll
+    for (int g = 0; g < CW; g += MG) {
+        if (g < nb) {
+            double a[S4][MG];
+#pragma unroll
+            for (int s = 0; s < S4; s++) {
+                if (s >= s_up) {
+                    if ((N & 1) == 0) {
+                        const double2 *p2 = reinterpret_cast<const double2 *>(lsrc[s] + g);
+#pragma unroll
+                        for (int h = 0; h < MG / 2; h++) {
+                            const double2 v = take[s] ? p2[h] : make_double2(0., 0.);
+                            a[s][2 * h] = v.x; a[s][2 * h + 1] = v.y;
+                        }
+                    } else {
+#pragma unroll
+                        for (int h = 0; h < MG; h++) a[s][h] = take[s] ? lsrc[s][g + h] : 0.;
+                    }
+                }
+            }
+#pragma unroll
+            for (int mm = 0; mm < MG; mm++) {
+                const int m = g + mm;
+                if (m < nb) {
+                    double u[CW];
+                    const double2 *up = reinterpret_cast<const double2 *>(&Ub[m][0]);
+#pragma unroll
+                    for (int j = 0; j < CW / 2; j++) { const double2 v = up[j]; u[2 * j] = v.x; u[2 * j + 1] = v.y; }
+#pragma unroll
+                    for (int s = 0; s < S4; s++) {
+                        if (s >= s_up) {
+#pragma unroll
+                            for (int c = 0; c < CW; c++) acc[s][c] = fma(-a[s][mm], u[c], acc[s][c]);
+                        }
+                    }
+                }
+            }
+        }
+    }
+    TACC(PH_GEMM, tg0);
+}
+
+// The factored chunk ci's participating rows to A (L below the pivots; the pivot rows with
+// L11 and U), perm / pos / b, and L11 of the chunk (strictly lower) to sm.pu.L11c[ci].
+__device__ __forceinline__ void lu3_publish(const double (&acc)[S4][CW], const int (&prow)[S4], int ci, int nb,
+                                            int s_lo, double *A, int N, double *b, const bool (&part)[S4],
+                                            const int (&lp)[S4], const double (&rb)[S4], Smem &sm) {
+    const int ln = threadIdx.x & 63, kk = ci * CW;
+#pragma unroll
+    for (int s = 0; s < S4; s++) {
+        const int r = 64 * s + ln;
+        if (s < s_lo || r >= N || !part[s]) continue;
+        const int p = prow[s], q = lp[s];
+        const double (&v)[CW] = acc[s];
+        if ((N & 1) == 0 && nb == CW) {
+            double2 *d2 = reinterpret_cast<double2 *>(A + (int64_t)p * N + kk);
+#pragma unroll
+            for (int j = 0; j < CW / 2; j++) d2[j] = make_double2(v[2 * j], v[2 * j + 1]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < CW; j++) if (j < nb) A[(int64_t)p * N + kk + j] = v[j];
+        }
+        sm.perm[kk + q] = p;
+        sm.pos[p] = kk + q;
+        b[p] = rb[s];
+#if !LVG_NARROW
+        if (q < nb) {
+#pragma unroll
+            for (int m = 0; m < CW; m++) sm.pu.L11c[ci][q][m] = m < q ? v[m] : 0.;
+        }
+#endif
+    }
+}
+
+__device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Smem &sm, const LuSrc &src, const bool FUSED) {
+    const int t = threadIdx.x;
+    for (int i = t; i < N; i += BT) {
+        sm.perm[i] = i;
+        sm.pos[i] = i;
+        if (FUSED) sm.resid[i] = (i == 0) ? 1. : 0.;
+    }
+    if (t == 0) { sm.seq = 0; sm.rdone = 0; }
+    __syncthreads();
+    const int l = t & 63, w = t >> 6;
+    const int nch = (N + CW - 1) / CW;
+    for (int j = w; j < nch; j += NW) {
+        const int c0 = j * CW;
+        const int nw = min(CW, N - c0);
+        TSTAMP(tp0);
+        // ---- a consistent snapshot of the tile -> physical row map: kp chunks are final
+        int prow[S4], kp;
+        for (;;) {
+            const int s1 = lu3_ld(sm.seq);
+            if (s1 & 1) { __builtin_amdgcn_s_sleep(1); continue; }
+#pragma unroll
+            for (int s = 0; s < S4; s++) prow[s] = (64 * s + l < N) ? sm.perm[64 * s + l] : 0;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (lu3_ld(sm.seq) == s1) { kp = s1 >> 1; break; }
+        }
+        const int SLO = (CW * kp) >> 6;             // slots below hold pivots of final chunks only
+        double acc[S4][CW];
+        // ---- this wave's chunk into registers (fused: assembled from K, the line terms and the
+        //      diagonal, row 0 <- 1)
+#pragma unroll
+        for (int s = 0; s < S4; s++) {
+            const int r = 64 * s + l, pr = prow[s];
+            const bool okr = r < N;
+            if (!FUSED) {
+#pragma unroll
+                for (int jj = 0; jj < CW; jj++) {
+                    const int d = c0 + jj;
+                    const bool ok = okr && jj < nw;
+                    double v;
+                    if (src.BK) {
+                        const double k = ok ? src.BK[(int64_t)pr * N + d] : 0.;
+                        const double e = (ok && pr < d) ? src.BE[(int64_t)d * N + pr] : 0.;
+                        const double dg = (ok && pr == d) ? src.BD[d] : 0.;
+                        v = (pr < d) ? 0.5 * e + k : k;   // build_collision_operators: 0.5 * af + dn
+                        if (pr == d) v = dg;
+                        if (pr == 0) v = 1.;
+                    } else {
+                        v = ok ? (src.B ? src.B : A)[(int64_t)pr * N + d] : 0.;
+                    }
+                    acc[s][jj] = ok ? v : 0.;
+                }
+            } else {
+                int li[CW];
+                const int64_t o = (int64_t)(okr ? pr : 0) * N + c0;
+                if ((N & 3) == 0 && nw == CW) {
+                    const double2 *k2 = reinterpret_cast<const double2 *>(src.K + o);
+                    const int4 *l4 = reinterpret_cast<const int4 *>(src.li + o);
+#pragma unroll
+                    for (int jj = 0; jj < CW / 2; jj++) {
+                        const double2 v = okr ? k2[jj] : make_double2(0., 0.);
+                        acc[s][2 * jj] = v.x; acc[s][2 * jj + 1] = v.y;
+                    }
+#pragma unroll
+                    for (int jj = 0; jj < CW / 4; jj++) {
+                        const int4 v = okr ? l4[jj] : make_int4(-1, -1, -1, -1);
+                        li[4 * jj] = v.x; li[4 * jj + 1] = v.y; li[4 * jj + 2] = v.z; li[4 * jj + 3] = v.w;
+                    }
+                } else {
+#pragma unroll
+                    for (int jj = 0; jj < CW; jj++) {
+                        const bool ok = okr && jj < nw;
+                        acc[s][jj] = ok ? src.K[o + jj] : 0.;
+                        li[jj] = ok ? src.li[o + jj] : -1;
+                    }
+                }
+#pragma unroll
+                for (int jj = 0; jj < CW; jj++) {
+                    const int d = c0 + jj;
+                    double v = acc[s][jj];
+                    if (li[jj] >= 0) v = v + src.y[li[jj]];
+                    if (pr == d) v = sm.diag[d < NMAX ? d : 0];
+                    if (pr == 0) v = 1.;
+                    acc[s][jj] = (okr && jj < nw) ? v : 0.;
+                    if (src.dump && okr && jj < nw) src.dump[(int64_t)pr * N + d] = v;
+                }
+            }
+        }
+        TACC(PH_BLOAD, tp0);
+        // ---- residual rows (physical), this chunk's columns in ascending order, chunks in turn
+        if (FUSED) {
+            TSTAMP(tr0);
+            lu3_wait(sm.rdone, j);
+#pragma unroll
+            for (int s = 0; s < S4; s++) {
+                const int r = 64 * s + l;
+                if (r < N) {
+                    double sr = sm.resid[prow[s]];
+#pragma unroll
+                    for (int jj = 0; jj < CW; jj++) if (jj < nw) sr = sr - acc[s][jj] * src.pop[c0 + jj];
+                    sm.resid[prow[s]] = sr;
+                }
+            }
+            wave_lds_sync();
+            if (l == 0) lu3_st(sm.rdone, j + 1);
+            TACC(PH_RSV, tr0);
+        }
+        // ---- the chunks before this one, in order, each once it is published
+        for (int ci = 0; ci < j; ci++) {
+            TSTAMP(tf0);
+            if (ci >= kp) lu3_wait(sm.seq, 2 * (ci + 1));
+            TACC(PH_T_FETCH, tf0);
+            const bool earlier = ci < kp;
+#if LVG_LU3_PRIO >= 2
+            if (ci == j - 1) __builtin_amdgcn_s_setprio(2);
+#endif
+            lu3_apply(acc, prow, earlier, ci, CW, earlier ? (CW * (ci + 1)) >> 6 : SLO, c0, nw, A, N, sm);
+        }
+        // ---- this chunk: factor, publish
+        const int nb = nw;
+        bool part[S4];
+        int lp[S4];
+        double rb[S4];
+        TSTAMP(tp1);
+#if LVG_LU3_PRIO >= 1
+        __builtin_amdgcn_s_setprio(2);
+#endif
+        lu2_panel(acc, prow, c0, nb, SLO, N, b, part, lp, rb, sm);
+        TACC(PH_PANEL, tp1);
+        TSTAMP(tw0);
+        if (l == 0) __hip_atomic_store(&sm.seq, 2 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        lu3_publish(acc, prow, j, nb, SLO, A, N, b, part, lp, rb, sm);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        wave_lds_sync();
+        if (l == 0) lu3_st(sm.seq, 2 * j + 2);
+#if LVG_LU3_PRIO >= 1
+        __builtin_amdgcn_s_setprio(0);
+#endif
+        TACC(PH_P_WB, tw0);
+    }
+    TSTAMP(tw1);
+    __syncthreads();
+    TACC(PH_BS_WAIT, tw1);
+    back_substitute(A, N, b, sm);
+    double emax = 0.;
+    if (FUSED && t < N) { const double r = sm.resid[t]; src.df[t] = r; emax = fabs(r); }
+    return FUSED ? block_max(emax, sm) : 0.;
+}
