@@ -463,7 +463,7 @@ def run_rank(args) -> int:
 
 
 KERNELS = {-1: "none (empty launch)", 0: "lvg::solve_kernel", 1: "lvg::solve_wave_kernel",
-           2: "lvg_wide::solve_kernel", 3: "lvg_big::solve_kernel", 4: "lvg_narrow::solve_kernel"}
+           2: "lvg_wide::solve_kernel", 3: "lvg_big::solve_kernel"}
 
 
 def report(args, world, N, total, L_cfg, lo, hi, units_total, units_local, nonconv, max_rel, max_layer_its,

@@ -341,9 +341,8 @@ int         lvg_last_coll_time(const lvg_handle *h, double *ms);
  * kernel gives bit-identical results): 0 the 256-thread block kernel (N <= 256), 1 the
  * wave kernel (N <= 64), 2 the 512-thread block kernel (N <= 256, launches with at most
  * two independent layers or one warm chain per CU), 3 the 768-thread block kernel
- * (N > 256), 4 the one-wave block kernel (N <= 256, launches with at least narrow_min
- * layers or chains per CU); -1 when nothing was launched (no solve yet, or an empty
- * batch). No reference counterpart. */
+ * (N > 256); -1 when nothing was launched (no solve yet, or an empty batch). No
+ * reference counterpart. */
 int         lvg_last_kernel_kind(const lvg_handle *h, int *kind);
 
 /* Tuning and diagnostics of this handle: "key=value,key=value", MERGED into the
@@ -356,10 +355,8 @@ int         lvg_last_kernel_kind(const lvg_handle *h, int *kind);
  * batch built ahead by a separate kernel), coll_mem (fraction of free device memory
  * that batch may take, default 0.5), coll_order (0: that kernel in layer order),
  * blocks_per_cu (resident block-kernel workgroups per CU, 0 = automatic), wide (0: never
- * the 512-thread kernel, 1: when the launch leaves CUs to spare, 2: always for N <= 256),
- * narrow (0: never the one-wave kernel, 1: when the launch has at least narrow_min items
- * per CU, 2: always for N <= 256 unless the 512-thread kernel applies), narrow_min (items
- * per CU, default 8). LVG_E_ARG on an unknown key or value (the tuning is then unchanged). No reference
+ * the 512-thread kernel, 1: when the launch leaves CUs to spare, 2: always for N <= 256).
+ * LVG_E_ARG on an unknown key or value (the tuning is then unchanged). No reference
  * counterpart (the reference has no device). */
 int         lvg_set_tuning(lvg_handle *h, const char *spec);
 

@@ -15,8 +15,8 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "_lib")
 LIB = os.path.join(LIB_DIR, "liblvg_amd.so")
-SOURCES = ["lvg_kernels.hip", "lvg_kernels_big.hip", "lvg_kernels_wide.hip", "lvg_kernels_narrow.hip", "lvg_wave.hip", "lvg_transitions.hip", "lvg_sched.hip", "lvg_abi.cpp"]
-HEADERS = ["lvg_device.h", "lvg_common.h", "lvg_lu256.h", "lvg_lu3.h", "lvg_kernels.hip", os.path.join("..", "..", "include", "lvg_amd.h"),
+SOURCES = ["lvg_kernels.hip", "lvg_kernels_big.hip", "lvg_kernels_wide.hip", "lvg_wave.hip", "lvg_transitions.hip", "lvg_sched.hip", "lvg_abi.cpp"]
+HEADERS = ["lvg_device.h", "lvg_common.h", "lvg_lu256.h", "lvg_kernels.hip", os.path.join("..", "..", "include", "lvg_amd.h"),
            os.path.join("..", "..", "include", "lvg_math.h")]
 ARCH = os.environ.get("LVG_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

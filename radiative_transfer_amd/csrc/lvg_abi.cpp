@@ -40,9 +40,6 @@ extern "C" hipError_t lvg_launch_lum(const LvgDevProblem *P, const LvgLaunch *L,
 // the 512-thread instantiation for underfilled launches at N <= 256 (lvg_kernels_wide.hip)
 extern "C" hipError_t lvg_launch_solve_wide(const LvgDevProblem *P, const LvgLaunch *L, int grid, hipStream_t s);
 extern "C" hipError_t lvg_kernel_occupancy_wide(int *blocks_per_cu);
-// the one-wave instantiation for launches with many layers per CU at N <= 256 (lvg_kernels_narrow.hip)
-extern "C" hipError_t lvg_launch_solve_narrow(const LvgDevProblem *P, const LvgLaunch *L, int grid, hipStream_t s);
-extern "C" hipError_t lvg_kernel_occupancy_narrow(int *blocks_per_cu);
 // the 768-thread instantiation for 256 < N <= 768 (lvg_kernels_big.hip)
 extern "C" hipError_t lvg_launch_solve_big(const LvgDevProblem *P, const LvgLaunch *L, int grid, hipStream_t s);
 extern "C" hipError_t lvg_launch_debug_big(const LvgDevProblem *P, const LvgLaunch *L, hipStream_t s);
@@ -85,9 +82,6 @@ struct LvgTuning {
     int coll_order = 1;        // coll_order=0: coll_kernel in layer order, not temperature order
     int blocks_per_cu = 0;     // blocks_per_cu=k: resident block-kernel workgroups per CU (0: automatic)
     int wide = 1;              // wide=0: never the 512-thread kernel; 1: when underfilled; 2: always (N <= 256)
-    int narrow = 0;            // narrow=0: never the one-wave kernel; 1: when the launch has at least
-                               // narrow_min items per CU; 2: always (N <= 256, unless wide applies)
-    int narrow_min = 8;        // narrow_min=k: items (layers or chains) per CU from which narrow=1 picks it
 };
 
 struct lvg_handle {
@@ -97,7 +91,6 @@ struct lvg_handle {
     int has_overlap = 0;
     int cus = 0, blocks_per_cu = 1;
     int wide_bpc = 0;              // resident 512-thread workgroups per CU (0: not available)
-    int narrow_bpc = 0;            // resident one-wave workgroups per CU (0: not available)
     int big = 0;                   // N > 256: the 768-thread block kernel (lvg_kernels_big.hip)
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evc = nullptr;   // evc: end of coll_kernel
@@ -110,7 +103,7 @@ struct lvg_handle {
     int *counter = nullptr;
     size_t lds_cap = 0;            // LDS bytes per workgroup (wave kernel plan)
     int last_kernel = -1;          // lvg_last_kernel_kind: -1 none (no launch yet, or an empty batch),
-                                   // 0 block, 1 wave, 2 512-thread, 3 768-thread, 4 one-wave kernel
+                                   // 0 block, 1 wave, 2 512-thread, 3 768-thread kernel
     // scratch for host-buffer solves
     double *d_soa = nullptr, *d_pops = nullptr;
     void *d_status = nullptr;
@@ -179,8 +172,6 @@ int parse_tuning(lvg_handle *h, const char *spec, LvgTuning &t) {
         else if (k == "coll_order") t.coll_order = x != 0.;
         else if (k == "blocks_per_cu" && x >= 0. && x <= 8.) t.blocks_per_cu = (int)x;
         else if (k == "wide" && (x == 0. || x == 1. || x == 2.)) t.wide = (int)x;
-        else if (k == "narrow" && (x == 0. || x == 1. || x == 2.)) t.narrow = (int)x;
-        else if (k == "narrow_min" && x >= 0. && x <= 64. && x == (int)x) t.narrow_min = (int)x;
         else return fail(h, LVG_E_ARG, "unknown tuning key or bad value '%s'", item.c_str());
     }
     return LVG_OK;
@@ -827,8 +818,6 @@ int lvg_create(const lvg_problem *prob, int device, lvg_handle **out) {
             h->blocks_per_cu = b;
             int bw = 0;
             if (!h->big && lvg_kernel_occupancy_wide(&bw) == hipSuccess) h->wide_bpc = std::min(bw, 1);
-            int bn = 0;
-            if (!h->big && lvg_kernel_occupancy_narrow(&bn) == hipSuccess) h->narrow_bpc = std::min(bn, 8);
         }
     }
     if (rc != LVG_OK) {
@@ -896,18 +885,11 @@ int launch_solve(lvg_handle *h, int nb_lay, const double *d_soa, double *d_pops,
     // between and halve each wave's update work. Bit-identical results.
     const bool wide = !wave && !h->big && h->wide_bpc >= 1 &&
                       (h->tune.wide == 2 || (h->tune.wide == 1 && nq <= (chain_off ? 1 : 2) * h->cus));
-    // the one-wave kernel (lvg_kernels_narrow.hip, N <= 256) when the launch has many items
-    // per CU: eight layers (or chains) per CU at once, each on its own wave with no barrier
-    // to any other, so every SIMD switches between two independent layers instead of
-    // waiting on one layer's pivot chain. Bit-identical results.
-    const bool narrow = !wave && !wide && !h->big && h->narrow_bpc >= 1 &&
-                        (h->tune.narrow == 2 || (h->tune.narrow == 1 && nq >= h->tune.narrow_min * h->cus));
     const int grid = wave ? std::max(1, std::min((nq + wpb - 1) / wpb, h->cus * wave_bpc))
                    : wide ? std::max(1, std::min(nq, h->cus * h->wide_bpc))
-                   : narrow ? std::max(1, std::min(nq, h->cus * h->narrow_bpc))
                           : std::max(1, std::min(nq, h->cus * per_cu));
     const int slots = wave ? grid * wpb : grid;
-    h->last_kernel = wave ? 1 : wide ? 2 : narrow ? 4 : h->big ? 3 : 0;
+    h->last_kernel = wave ? 1 : wide ? 2 : h->big ? 3 : 0;
     if ((rc = ensure_workspace(h, slots))) return rc;
     LvgLaunch L;
     fill_launch(h, L, o);
@@ -1000,7 +982,6 @@ int launch_solve(lvg_handle *h, int nb_lay, const double *d_soa, double *d_pops,
     }
     if (wave) HIPCHECK(h, lvg_launch_solve_wave(h->d_prob, dL, h->N, grid, wpb, wdyn, s));
     else if (wide) HIPCHECK(h, lvg_launch_solve_wide(h->d_prob, dL, grid, s));
-    else if (narrow) HIPCHECK(h, lvg_launch_solve_narrow(h->d_prob, dL, grid, s));
     else HIPCHECK(h, h->big ? lvg_launch_solve_big(h->d_prob, dL, grid, s) : lvg_launch_solve(h->d_prob, dL, grid, s));
     HIPCHECK(h, hipEventRecord(h->ev1, s));
     h->last_launches = 1;

@@ -267,10 +267,7 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
     const int N = P.N, t = threadIdx.x;
     const double T = sm.T, Te = sm.Te;
     const int nt = (N + 15) >> 4, ntiles = nt * (nt + 1) / 2;
-    // BTH < 256 (one-wave instantiation): the tiles are walked VB times, each pass a band of
-    // BTH / 16 tile rows (pairs and stores as for 256 threads, in another order)
-    constexpr int VB = BTH >= 256 ? 1 : 256 / BTH;
-    const int sl = t & 15;
+    const int fl = (t >> 4) & 15, sl = t & 15;
     TSTAMP(tq0);
     const int M = N * (N - 1) / 2;
     if (cls_lds) {
@@ -280,8 +277,8 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
         for (int e = (n16 << 4) + t; e < M; e += BTH) cls_lds[e] = P.pair_class[e];
         __syncthreads();
     }
-    constexpr int TG = BTH >= 256 ? BTH / 256 : 1;   // TG groups of 256 threads, PU tiles each
-    const int tg = BTH >= 256 ? t >> 8 : 0;
+    constexpr int TG = BTH / 256;                    // TG groups of 256 threads, PU tiles each
+    const int tg = t >> 8;
     double wk0[PU], wk1[PU], wb0[PU], wb1[PU];
     int wf[PU], ws[PU];
 #pragma unroll
@@ -300,9 +297,7 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
             }
         }
     };
-    for (int vb = 0; vb < VB; vb++)
     for (int q0 = 0; q0 < ntiles; q0 += PU * TG) {
-        const int fl = BTH >= 256 ? (t >> 4) & 15 : (t >> 4) + (16 / VB) * vb;
         int pc[PU], fc[PU], sc[PU], cls[PU];
 #pragma unroll
         for (int u = 0; u < PU; u++) {

@@ -39,18 +39,12 @@
 #ifndef LVG_WIDE
 #define LVG_WIDE 0
 #endif
-#ifndef LVG_NARROW
-#define LVG_NARROW 0
-#endif
 #if LVG_BIG
 #define LVG_NS lvg_big
 #define LVG_SYM(name) name##_big
 #elif LVG_WIDE
 #define LVG_NS lvg_wide
 #define LVG_SYM(name) name##_wide
-#elif LVG_NARROW
-#define LVG_NS lvg_narrow
-#define LVG_SYM(name) name##_narrow
 #else
 #define LVG_NS lvg
 #define LVG_SYM(name) name
@@ -68,30 +62,20 @@ namespace LVG_NS {
     atomicAdd(&lvg_ph_lds[ph], t_ - (v0)); } } while (0)
 #endif
 
-constexpr int BT   = LVG_BIG ? 768 : LVG_WIDE ? 512 : LVG_NARROW ? 64 : 256;   // threads per workgroup
+constexpr int BT   = LVG_BIG ? 768 : LVG_WIDE ? 512 : 256;   // threads per workgroup
 constexpr int NMAX = LVG_BIG ? 768 : 256;   // max levels of this kernel
 #ifndef LVG_OCC
 #define LVG_OCC (LVG_BIG || LVG_WIDE ? 1 : 2)
 #endif
 // the second __launch_bounds__ argument: waves per SIMD the register allocation is built for
-// (amdgpu-waves-per-eu; 2 -> 256 registers a wave): two 4-wave workgroups per CU for the
-// 256-thread kernel, eight one-wave workgroups per CU for the narrow one
+// (amdgpu-waves-per-eu; 2 -> 256 registers a wave: two 4-wave workgroups per CU for the
+// 256-thread kernel; the 512- and 768-thread kernels are bounded by their workgroup size)
 constexpr int OCC  = LVG_OCC;
-#ifndef LVG_LU_CW
-#define LVG_LU_CW 16
-#endif
-#ifndef LVG_LU3
-#define LVG_LU3 LVG_NARROW
-#endif
-constexpr int LU_CW = LVG_LU_CW;            // N <= 256 LU: columns per wave (lvg_lu256.h)
+constexpr int LU_CW = 16;                   // N <= 256 LU: columns per chunk (lvg_lu256.h)
 constexpr int NW   = BT / 64;
 constexpr int NB   = 16;                    // LU panel width (chunk)
-static_assert((LVG_NARROW || NMAX <= BT) && BT % 64 == 0 && NMAX % 32 == 0, "at least one row per thread, whole waves");
-static_assert(!LVG_NARROW || LVG_LU3, "the one-wave instantiation runs the chunk-pipelined LU");
-#ifndef LVG_YCAP
-#define LVG_YCAP (LVG_NARROW ? 1 : 2048)
-#endif
-constexpr int YCAP = LVG_BIG ? 1 : LVG_YCAP;    // line terms kept in LDS when 2*nb_lines <= YCAP
+static_assert(NMAX <= BT && BT % 64 == 0 && NMAX % 32 == 0, "at least one row per thread, whole waves");
+constexpr int YCAP = LVG_BIG ? 1 : 2048;    // line terms kept in LDS when 2*nb_lines <= YCAP    // line terms kept in LDS when 2*nb_lines <= YCAP
 constexpr int TC = 4;                       // columns per thread in the LU register tile (TR rows x TC)
 constexpr int TR = NMAX * 8 / BT;           // tile rows per thread: the BT/8 row groups cover NMAX
 static_assert(TR * (BT / 8) >= NMAX && TR % 2 == 0, "the register tiles cover every row");
@@ -133,16 +117,10 @@ struct Smem {
     double red[NW];
     alignas(16) double L11[NB][NB + 1];    // unit-lower diagonal block of the current chunk
     alignas(16) double Ub[NW][LU_CW][LU_CW];   // per wave: the chunk's pivot rows in its columns, then U
-#if LVG_LU3
     int seq;                    // LU chunk sequence: 2 x chunks published (odd while one is published)
     int rdone;                  // chunks whose columns the residual has taken
-#endif
     union alignas(16) {
-#if LVG_LU3 && !LVG_NARROW
         double L11c[NMAX / LU_CW][LU_CW][LU_CW + 1];   // unit-lower diagonal block of every chunk
-#elif !LVG_LU3
-        double Lst[LU_CW][NMAX];   // L of the current chunk by tile row, 0 where a row takes no update
-#endif
         double hist_acc[32];    // accel_step sums (used outside the LU only)
     } pu;
 #endif
@@ -260,60 +238,6 @@ struct LuSrc {
     const double *BK = nullptr, *BE = nullptr, *BD = nullptr;
 };
 
-#if LVG_NARROW
-// ---- back substitution U x = y for the one-wave instantiation: per block of NB rows from
-//      the bottom, the diagonal block solved in registers (lane r < nb: b_r and row r of the
-//      block from A; x_m broadcast by DPP row_newbcast:m, as below), then the rows above
-//      updated, each lane several rows; every entry takes its updates for k descending.
-__device__ __forceinline__ void back_substitute(const double *A, int N, const double *b, Smem &sm) {
-    const int t = threadIdx.x;
-    TSTAMP(tb0);
-    for (int i = t; i < N; i += BT) sm.blog[i] = b[sm.perm[i]];
-    __syncthreads();
-    const int nblk = (N + NB - 1) / NB;
-    for (int kb = nblk - 1; kb >= 0; kb--) {
-        const int k0 = kb * NB, nb = min(NB, N - k0);
-        {
-            const int r = t & 15;
-            double bt = (t < nb) ? sm.blog[k0 + t] : 0., ur[NB];
-            const double *drow = A + (int64_t)sm.perm[k0 + (t < nb ? t : 0)] * N + k0;
-#pragma unroll
-            for (int m = 0; m < NB; m++) ur[m] = (t < nb && m < nb) ? drow[m] : 1.;
-#define LVG_BSUB_STEP(M_)                                                                  \
-            if ((M_) < nb) {                                                               \
-                const double xm = dpp_d<0x150 + (M_), 0xf, 0xf>(bt / ur[M_]);              \
-                if (r < (M_)) bt = fma(-ur[M_], xm, bt);                                   \
-                else if (r == (M_)) bt = xm;                                               \
-            }
-            LVG_BSUB_STEP(15) LVG_BSUB_STEP(14) LVG_BSUB_STEP(13) LVG_BSUB_STEP(12)
-            LVG_BSUB_STEP(11) LVG_BSUB_STEP(10) LVG_BSUB_STEP(9) LVG_BSUB_STEP(8)
-            LVG_BSUB_STEP(7) LVG_BSUB_STEP(6) LVG_BSUB_STEP(5) LVG_BSUB_STEP(4)
-            LVG_BSUB_STEP(3) LVG_BSUB_STEP(2) LVG_BSUB_STEP(1) LVG_BSUB_STEP(0)
-#undef LVG_BSUB_STEP
-            if (t < nb) sm.blog[k0 + t] = bt;
-        }
-        __syncthreads();
-        for (int row = t; row < k0; row += BT) {
-            double s = sm.blog[row], u[NB];
-            const double *urow = A + (int64_t)sm.perm[row] * N + k0;
-            if ((N & 1) == 0 && nb == NB) {
-                const double2 *r2 = reinterpret_cast<const double2 *>(urow);
-#pragma unroll
-                for (int m = 0; m < NB / 2; m++) { const double2 v = r2[m]; u[2 * m] = v.x; u[2 * m + 1] = v.y; }
-            } else {
-#pragma unroll
-                for (int m = 0; m < NB; m++) u[m] = (m < nb) ? urow[m] : 0.;
-            }
-#pragma unroll
-            for (int m = NB - 1; m >= 0; m--)
-                if (m < nb) s = fma(-u[m], sm.blog[k0 + m], s);
-            sm.blog[row] = s;
-        }
-        __syncthreads();
-    }
-    TACC(PH_BACKSUB, tb0);
-}
-#else
 // ---- back substitution U x = y in logical order, blocked by NB from the bottom:
 //      wave 0 solves the diagonal block in registers, then all threads update the
 //      rows above; every entry receives its updates for k descending (oracle order).
@@ -394,7 +318,6 @@ __device__ __forceinline__ void back_substitute(const double *A, int N, const do
     }
     TACC(PH_BACKSUB, tb0);
 }
-#endif
 
 #if LVG_BIG
 // ------------------------------------------------------------------------------
@@ -1266,7 +1189,7 @@ __global__ void __launch_bounds__(64) lum_reduce_kernel(const LvgLumArgs *__rest
     A.lum[tr] = s / A.height;
 }
 
-#if !LVG_BIG && !LVG_WIDE && !LVG_NARROW
+#if !LVG_BIG && !LVG_WIDE
 // ---- collision operators of a whole batch of layers, ahead of the solve ----------------
 // build_collision_operators for every layer of the launch into K_all / B_all (HBM), with
 // a small LDS footprint (layer scalars and the rule table only) so that many workgroups
@@ -1346,7 +1269,7 @@ extern "C" hipError_t LVG_SYM(lvg_launch_solve)(const LvgDevProblem *P, const Lv
     return hipGetLastError();
 }
 
-#if !LVG_BIG && !LVG_WIDE && !LVG_NARROW
+#if !LVG_BIG && !LVG_WIDE
 extern "C" hipError_t lvg_launch_coll(const LvgDevProblem *P, const LvgLaunch *L, int grid, hipStream_t s) {
     hipLaunchKernelGGL(lvg::coll_kernel, dim3(grid), dim3(lvg::BT), 0, s, P, L);
     return hipGetLastError();

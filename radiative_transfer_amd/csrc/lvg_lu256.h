@@ -1,36 +1,36 @@
 // lvg_lu256.h — the LU of calc_new_pop / boundary_layer_populations for N <= 256 (the
-// 256-thread solve_kernel), included by lvg_kernels.hip inside namespace lvg.
+// 256- and 512-thread solve_kernel), included by lvg_kernels.hip inside its namespace.
 //
 // lu_matrix_solve (absent library; call sites iteration_lvg.cpp:100, iteration_control.cpp:87)
-// as a left-looking blocked LU with partial pivoting, b eliminated alongside, in which
-// every wave OWNS COLUMNS:
-//  * Block columns of 16 x (waves): 64 for the 256-thread kernel, 128 for the 512-thread
-//    one (LVG_WIDE); wave w holds columns c0 + 16w .. c0 + 16w + 15 of every row in
-//    registers: lane l keeps tile rows 64 s + l (s < 4, logical order as of the block
-//    load), acc[s][0..16) — 128 fp64 registers.
-//  * An earlier chunk kk (16 columns of L, final) is staged once per workgroup into LDS
-//    by tile row (Lst[m][row]); each wave then solves the chunk's 16 pivot rows in ITS
-//    columns (TRSM against L11 in a 4 x 16-lane layout, DPP row broadcasts) and updates
-//    its rows below with L (LDS) and U (its own LDS rows, broadcast reads). The waves do
-//    identical work, so the two barriers of a step cost little; rows above the chunk
-//    drop out in whole 64-row slots, for every wave alike.
-//  * The block's own chunks are factored by the wave that owns them, alone in its
-//    registers (pivot by DPP max over 4 rows per lane + ballot, pivot row by readlane):
-//    no barrier per column. Its L is published through the same LDS stage, and the
-//    waves to its right apply it (TRSM + update) while the next owner factors.
-//  * The residual df = e0 - A n of the fused assembly runs row by row in column order,
-//    handed from wave to wave through LDS (one barrier per wave per block column).
-// Every element receives fma(-l_ik, u_kj, a_ij) for k ascending and the pivots are chosen
-// from identical values with the oracle's rule (largest |v|, first maximum in logical
-// order, NaN diagonal kept), so the factors, the solution and the residual equal the
-// unblocked, physically pivoting oracle_lu_solve bit for bit. On return sm.blog holds x.
-// b: LDS [N] indexed by physical row.
+// as a left-looking LU over chunks of CW = 16 columns, chunk j owned by wave j mod NW, with
+// no workgroup barrier between chunks:
+//  * A wave takes its next chunk as soon as it has published the previous one: it loads the
+//    chunk's columns (assembled from K, the line terms and the diagonal when fused) for the
+//    tile rows of a consistent snapshot of the row permutation (seqlock on sm.seq: positions
+//    of published chunks are final, so their rows sit at their own tile rows), adds the
+//    chunk's columns to the residual in column order (chunks in turn, sm.rdone), then
+//    applies chunks 0 .. j-1 in order, waiting only for those not yet published, and factors
+//    the chunk (lu_panel) and publishes it.
+//  * Applying chunk i: the chunk's pivot rows in this wave's columns are solved against
+//    L11 of chunk i (kept in LDS for every chunk, sm.pu.L11c) and stored as U rows; the rows
+//    below take the rank-16 update with L read straight from the factors in A (4 columns of
+//    L at a time), U broadcast from the wave's LDS rows.
+//  * Publishing chunk j: L and the pivot rows to A, perm / pos / b, L11 of the chunk, then
+//    sm.seq = 2 (j + 1) behind a workgroup release fence.
+// So while the owner of chunk j factors it, the other waves already apply the published
+// chunks to their next chunks instead of waiting at a barrier; the chain is panel j ->
+// apply of j to chunk j+1 -> panel j+1.
+// Every element still receives fma(-l_ik, u_kj, a_ij) for k ascending and the pivots are
+// those of lu_panel (the oracle's rule), so the results are the unblocked oracle's bit for
+// bit. On return sm.blog holds x.
+
+// Rows: lane l of every wave keeps tile rows 64 s + l (s < 4) of its chunk, acc[s][0..16)
+// (128 fp64 registers); b: LDS [N] indexed by physical row.
 
 constexpr int S4 = NMAX / 64;   // row slots per lane: tile row 64 s + lane
-constexpr int CW = LU_CW;       // columns per wave = chunk (panel) width: 16 or 8
-constexpr int BW = NW * CW;     // block-column width: 64 (4 waves) or 128 (8 waves, LVG_WIDE)
+constexpr int CW = LU_CW;       // chunk (panel) width
 constexpr int CL = CW / 4;      // TRSM columns per lane (4 x 16-lane rows)
-static_assert(CW == 16 || CW == 8, "chunk width: the TRSM lays 16 rows over 16-lane groups");
+static_assert(CW == 16, "chunk width: the TRSM lays the 16 rows of a chunk over 16-lane groups");
 
 // LDS stores of one lane visible to the other lanes of its wave: a wave's LDS instructions
 // execute in issue order, so only compiler motion has to be stopped (wavefront-scope
@@ -42,88 +42,6 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-#if !LVG_LU3
-// One chunk applied to this wave's columns: the chunk's pivot rows (tile rows kk.. for an
-// earlier chunk, the rows whose logical position is kk.. for one of this block) published
-// by their owner lanes to Ub[w], solved against L11 (x_r takes its updates for m ascending,
-// x_m broadcast within the 16-lane row by DPP row_share), written back as U rows and
-// stored to A; then the rows of slots >= s_lo updated with Lst (0 where a row takes no
-// update) and those U rows, m ascending.
-__device__ __forceinline__ void lu2_apply(double (&acc)[S4][CW], const int (&prow)[S4], bool earlier, int kk, int nb,
-                                          int s_lo, int cw0, int nw, double *A, int N, Smem &sm) {
-    const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-    double (*Ub)[CW] = sm.Ub[w];
-    TSTAMP(ta0);
-#pragma unroll
-    for (int s = 0; s < S4; s++) {
-        const int r = 64 * s + l;
-        if (r < N) {
-            const int q = (earlier ? r : sm.pos[prow[s]]) - kk;
-            if (q >= 0 && q < nb) {
-                double2 *d = reinterpret_cast<double2 *>(&Ub[q][0]);
-#pragma unroll
-                for (int j = 0; j < CW / 2; j++) d[j] = make_double2(acc[s][2 * j], acc[s][2 * j + 1]);
-            }
-        }
-    }
-    wave_lds_sync();
-    {
-        const int q4 = l >> 4, r = l & 15;        // lane: row r of the chunk, columns CL*q4..
-        double x[CL];
-        if (r < CW) {
-#pragma unroll
-            for (int i = 0; i < CL; i++) x[i] = Ub[r][CL * q4 + i];
-        }
-        const double *lrw = sm.L11[r < CW ? r : 0];
-#define LVG_TRSM_STEP(M_)                                                                  \
-        if ((M_) < nb - 1) {                                                               \
-            const double lm = lrw[M_];                                                     \
-            _Pragma("unroll") for (int i = 0; i < CL; i++) {                               \
-                const double y = dpp_d<0x150 + (M_), 0xf, 0xf>(x[i]);                      \
-                if (r > (M_)) x[i] = fma(-lm, y, x[i]);                                    \
-            }                                                                              \
-        }
-        LVG_TRSM_STEP(0) LVG_TRSM_STEP(1) LVG_TRSM_STEP(2) LVG_TRSM_STEP(3)
-        LVG_TRSM_STEP(4) LVG_TRSM_STEP(5) LVG_TRSM_STEP(6) LVG_TRSM_STEP(7)
-        LVG_TRSM_STEP(8) LVG_TRSM_STEP(9) LVG_TRSM_STEP(10) LVG_TRSM_STEP(11)
-        LVG_TRSM_STEP(12) LVG_TRSM_STEP(13) LVG_TRSM_STEP(14)
-#undef LVG_TRSM_STEP
-        if (r < nb) {
-#pragma unroll
-            for (int i = 0; i < CL; i++) Ub[r][CL * q4 + i] = x[i];
-            double *urow = A + (int64_t)sm.perm[kk + r] * N + cw0 + CL * q4;
-#pragma unroll
-            for (int i = 0; i < CL; i++) if (CL * q4 + i < nw) urow[i] = x[i];
-        }
-    }
-    wave_lds_sync();
-    TACC(PH_T_SOLVE, ta0);
-    TSTAMP(tg0);
-    for (int m = 0; m < nb; m++) {
-        double u[CW];
-        const double2 *up = reinterpret_cast<const double2 *>(&Ub[m][0]);
-#pragma unroll
-        for (int j = 0; j < CW / 2; j++) { const double2 v = up[j]; u[2 * j] = v.x; u[2 * j + 1] = v.y; }
-        // every slot's L read with the U row (one LDS wait per m, not one per slot): the
-        // asm use keeps the reads from being sunk into the slot branches
-        double a[S4];
-#pragma unroll
-        for (int s = 0; s < S4; s++) a[s] = sm.pu.Lst[m][64 * s + l];
-        static_assert(S4 == 4, "four row slots");
-        asm volatile("" :: "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]));
-#pragma unroll
-        for (int s = 0; s < S4; s++) {
-            if (s >= s_lo) {
-#pragma unroll
-                for (int c = 0; c < CW; c++) acc[s][c] = fma(-a[s], u[c], acc[s][c]);
-            }
-        }
-    }
-    TACC(PH_GEMM, tg0);
-}
-
-#endif
-
 // The chunk kk (this wave's CW columns) factored by this wave alone: rows of slots >= s_lo
 // whose logical position is >= kk take part (exec-masked), 4 rows per lane. Per column:
 // the lane's best key over its rows, one DPP wave max + ballot (lower word and position
@@ -133,9 +51,9 @@ __device__ __forceinline__ void lu2_apply(double (&acc)[S4][CW], const int (&pro
 // The row select is a v_cndmask chain: written as branches on the (uniform) slot, or
 // through LDS, the compiler folds it into a dynamic acc[ss] index and moves acc to
 // scratch memory (measured: 352 -> 800 B/lane).
-__device__ __forceinline__ void lu2_panel(double (&acc)[S4][CW], const int (&prow)[S4], int kk, int nb, int s_lo,
-                                             int N, const double *b, bool (&part)[S4], int (&lp)[S4],
-                                             double (&rb)[S4], Smem &sm) {
+__device__ __forceinline__ void lu_panel(double (&acc)[S4][CW], const int (&prow)[S4], int kk, int nb, int s_lo,
+                                         int N, const double *b, bool (&part)[S4], int (&lp)[S4],
+                                         double (&rb)[S4], Smem &sm) {
     const int ln = threadIdx.x & 63;
     bool act[S4];
 #pragma unroll
@@ -238,83 +156,152 @@ __device__ __forceinline__ void lu2_panel(double (&acc)[S4][CW], const int (&pro
     }
 }
 
-#if !LVG_LU3
-// The factored chunk's rows (logical position >= kk) to A (L below the pivots; the pivot
-// rows with L11 and U), perm/pos/b, L11 (strictly lower) and the
-// stage Lst (L of the rows below the chunk, 0 for the others) for the waves to its right.
-__device__ __forceinline__ void lu2_publish(const double (&acc)[S4][CW], const int (&prow)[S4], int kk, int nb,
+__device__ __forceinline__ int lu_ld(const int &x) {
+    return __hip_atomic_load(&x, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lu_st(int &x, int v) {
+    __hip_atomic_store(&x, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// the wave waits (sleeping between polls) until the sequence word reaches v
+__device__ __forceinline__ void lu_wait(const int &x, int v) {
+    while (lu_ld(x) < v) __builtin_amdgcn_s_sleep(1);
+}
+
+// Chunk ci (columns kk.., nb of them, published) applied to this wave's columns cw0.. (nw).
+// earlier: ci was published before this chunk's load, so its pivot rows sit at tile rows
+// kk..kk+15 and the rows taking its update at tile rows >= kk + 16. s_up: first row slot
+// that can hold a row taking an update (tile rows below 16 x the chunks final at the load
+// are pivots of earlier chunks).
+__device__ __forceinline__ void lu_apply(double (&acc)[S4][CW], const int (&prow)[S4], bool earlier, int ci, int nb,
+                                         int s_up, int cw0, int nw, double *A, int N, Smem &sm) {
+    const int l = threadIdx.x & 63, w = threadIdx.x >> 6, kk = ci * CW;
+    double (*Ub)[CW] = sm.Ub[w];
+    TSTAMP(ta0);
+    // the chunk's pivot rows in this wave's columns to Ub (their owner lanes)
+#pragma unroll
+    for (int s = 0; s < S4; s++) {
+        const int r = 64 * s + l;
+        if (s >= (earlier ? kk >> 6 : s_up) && r < N) {
+            const int q = (earlier ? r : sm.pos[prow[s]]) - kk;
+            if (q >= 0 && q < nb) {
+                double2 *d = reinterpret_cast<double2 *>(&Ub[q][0]);
+#pragma unroll
+                for (int j = 0; j < CW / 2; j++) d[j] = make_double2(acc[s][2 * j], acc[s][2 * j + 1]);
+            }
+        }
+    }
+    wave_lds_sync();
+    {
+        const int q4 = l >> 4, r = l & 15;        // lane: row r of the chunk, columns CL*q4..
+        double x[CL];
+        if (r < CW) {
+#pragma unroll
+            for (int i = 0; i < CL; i++) x[i] = Ub[r][CL * q4 + i];
+        }
+        const double *lrw = sm.pu.L11c[ci][r < CW ? r : 0];
+#define LVG_TRSM_STEP(M_)                                                                  \
+        if ((M_) < nb - 1) {                                                               \
+            const double lm = lrw[M_];                                                     \
+            _Pragma("unroll") for (int i = 0; i < CL; i++) {                               \
+                const double y = dpp_d<0x150 + (M_), 0xf, 0xf>(x[i]);                      \
+                if (r > (M_)) x[i] = fma(-lm, y, x[i]);                                    \
+            }                                                                              \
+        }
+        LVG_TRSM_STEP(0) LVG_TRSM_STEP(1) LVG_TRSM_STEP(2) LVG_TRSM_STEP(3)
+        LVG_TRSM_STEP(4) LVG_TRSM_STEP(5) LVG_TRSM_STEP(6) LVG_TRSM_STEP(7)
+        LVG_TRSM_STEP(8) LVG_TRSM_STEP(9) LVG_TRSM_STEP(10) LVG_TRSM_STEP(11)
+        LVG_TRSM_STEP(12) LVG_TRSM_STEP(13) LVG_TRSM_STEP(14)
+#undef LVG_TRSM_STEP
+        if (r < nb) {
+#pragma unroll
+            for (int i = 0; i < CL; i++) Ub[r][CL * q4 + i] = x[i];
+            double *urow = A + (int64_t)sm.perm[kk + r] * N + cw0 + CL * q4;
+#pragma unroll
+            for (int i = 0; i < CL; i++) if (CL * q4 + i < nw) urow[i] = x[i];
+        }
+    }
+    wave_lds_sync();
+    TACC(PH_T_SOLVE, ta0);
+    TSTAMP(tg0);
+    // rows taking the update: below the chunk's pivots (logical position >= kk + nb)
+    bool take[S4];
+    const double *lsrc[S4];
+#pragma unroll
+    for (int s = 0; s < S4; s++) {
+        const int r = 64 * s + l;
+        take[s] = s >= s_up && r < N && (earlier ? r : sm.pos[prow[s]]) >= kk + nb;
+        lsrc[s] = A + (int64_t)(take[s] ? prow[s] : 0) * N + kk;
+    }
+    constexpr int MG = 4;                         // columns of L per load group
+#pragma unroll
+    for (int g = 0; g < CW; g += MG) {
+        if (g < nb) {
+            double a[S4][MG];
+#pragma unroll
+            for (int s = 0; s < S4; s++) {
+                if (s >= s_up) {
+                    if ((N & 1) == 0) {
+                        const double2 *p2 = reinterpret_cast<const double2 *>(lsrc[s] + g);
+#pragma unroll
+                        for (int h = 0; h < MG / 2; h++) {
+                            const double2 v = take[s] ? p2[h] : make_double2(0., 0.);
+                            a[s][2 * h] = v.x; a[s][2 * h + 1] = v.y;
+                        }
+                    } else {
+#pragma unroll
+                        for (int h = 0; h < MG; h++) a[s][h] = take[s] ? lsrc[s][g + h] : 0.;
+                    }
+                }
+            }
+#pragma unroll
+            for (int mm = 0; mm < MG; mm++) {
+                const int m = g + mm;
+                if (m < nb) {
+                    double u[CW];
+                    const double2 *up = reinterpret_cast<const double2 *>(&Ub[m][0]);
+#pragma unroll
+                    for (int j = 0; j < CW / 2; j++) { const double2 v = up[j]; u[2 * j] = v.x; u[2 * j + 1] = v.y; }
+#pragma unroll
+                    for (int s = 0; s < S4; s++) {
+                        if (s >= s_up) {
+#pragma unroll
+                            for (int c = 0; c < CW; c++) acc[s][c] = fma(-a[s][mm], u[c], acc[s][c]);
+                        }
+                    }
+                }
+            }
+        }
+    }
+    TACC(PH_GEMM, tg0);
+}
+
+// The factored chunk ci's participating rows to A (L below the pivots; the pivot rows with
+// L11 and U), perm / pos / b, and L11 of the chunk (strictly lower) to sm.pu.L11c[ci].
+__device__ __forceinline__ void lu_publish(const double (&acc)[S4][CW], const int (&prow)[S4], int ci, int nb,
                                             int s_lo, double *A, int N, double *b, const bool (&part)[S4],
                                             const int (&lp)[S4], const double (&rb)[S4], Smem &sm) {
-    const int ln = threadIdx.x & 63;
+    const int ln = threadIdx.x & 63, kk = ci * CW;
 #pragma unroll
     for (int s = 0; s < S4; s++) {
         const int r = 64 * s + ln;
-        if (s < s_lo || r >= N) continue;
-        if (part[s]) {
-            const int p = prow[s], q = lp[s];
-            const bool piv = q < nb;
-            const double (&v)[CW] = acc[s];
-            if ((N & 1) == 0 && nb == CW) {
-                double2 *d2 = reinterpret_cast<double2 *>(A + (int64_t)p * N + kk);
+        if (s < s_lo || r >= N || !part[s]) continue;
+        const int p = prow[s], q = lp[s];
+        const double (&v)[CW] = acc[s];
+        if ((N & 1) == 0 && nb == CW) {
+            double2 *d2 = reinterpret_cast<double2 *>(A + (int64_t)p * N + kk);
 #pragma unroll
-                for (int j = 0; j < CW / 2; j++) d2[j] = make_double2(v[2 * j], v[2 * j + 1]);
-            } else {
-#pragma unroll
-                for (int j = 0; j < CW; j++) if (j < nb) A[(int64_t)p * N + kk + j] = v[j];
-            }
-            sm.perm[kk + q] = p;
-            sm.pos[p] = kk + q;
-            b[p] = rb[s];
-            if (piv) {
-#pragma unroll
-                for (int m = 0; m < CW; m++) { sm.L11[q][m] = m < q ? v[m] : 0.; sm.pu.Lst[m][r] = 0.; }
-            } else {
-#pragma unroll
-                for (int m = 0; m < CW; m++) sm.pu.Lst[m][r] = m < nb ? v[m] : 0.;
-            }
+            for (int j = 0; j < CW / 2; j++) d2[j] = make_double2(v[2 * j], v[2 * j + 1]);
         } else {
 #pragma unroll
-            for (int m = 0; m < CW; m++) sm.pu.Lst[m][r] = 0.;
+            for (int j = 0; j < CW; j++) if (j < nb) A[(int64_t)p * N + kk + j] = v[j];
         }
-    }
-}
-
-// L of earlier chunk kk for tile row t (= logical row t: the pivots of earlier blocks are
-// final at this block's load): the row's 16 values from A when t >= kk, else zeros
-__device__ __forceinline__ void lu2_fetch_l(const double *A, int N, int kk, int trow, double (&pf)[CW]) {
-    const int t = threadIdx.x;
-    const bool need = t < N && t >= kk;
-    const double *src = A + (int64_t)(need ? trow : 0) * N + kk;
-    if ((N & 1) == 0) {
-        const double2 *s2 = reinterpret_cast<const double2 *>(src);
+        sm.perm[kk + q] = p;
+        sm.pos[p] = kk + q;
+        b[p] = rb[s];
+        if (q < nb) {
 #pragma unroll
-        for (int j = 0; j < CW / 2; j++) {
-            const double2 v = need ? s2[j] : make_double2(0., 0.);
-            pf[2 * j] = v.x;
-            pf[2 * j + 1] = v.y;
+            for (int m = 0; m < CW; m++) sm.pu.L11c[ci][q][m] = m < q ? v[m] : 0.;
         }
-    } else {
-#pragma unroll
-        for (int j = 0; j < CW; j++) pf[j] = need ? src[j] : 0.;
-    }
-}
-
-// ... into the stage: rows below the chunk keep their 16 values; the chunk's own rows go
-// to L11 (strictly lower part) and stage zeros, as do the rows above
-__device__ __forceinline__ void lu2_stage_l(int N, int kk, const double (&pf)[CW], Smem &sm) {
-    const int t = threadIdx.x;
-    if (t >= N) return;
-    if (t >= kk + CW) {
-#pragma unroll
-        for (int m = 0; m < CW; m++) sm.pu.Lst[m][t] = pf[m];
-    } else {
-        if (t >= kk) {
-            const int q = t - kk;
-#pragma unroll
-            for (int m = 0; m < CW; m++) sm.L11[q][m] = m < q ? pf[m] : 0.;
-        }
-#pragma unroll
-        for (int m = 0; m < CW; m++) sm.pu.Lst[m][t] = 0.;
     }
 }
 
@@ -325,30 +312,37 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
         sm.pos[i] = i;
         if (FUSED) sm.resid[i] = (i == 0) ? 1. : 0.;
     }
+    if (t == 0) { sm.seq = 0; sm.rdone = 0; }
     __syncthreads();
     const int l = t & 63, w = t >> 6;
-    for (int c0 = 0; c0 < N; c0 += BW) {
-        const int SLO = c0 >> 6;                  // slots above this block's rows hold earlier pivots
+    const int nch = (N + CW - 1) / CW;
+    for (int j = w; j < nch; j += NW) {
+        const int c0 = j * CW;
+        const int nw = min(CW, N - c0);
         TSTAMP(tp0);
-        const int wJ = min(BW, N - c0);
-        const int cw0 = c0 + CW * w;                  // this wave's first column
-        const int nw = max(0, min(CW, wJ - CW * w));  // ... and how many it has
-        int prow[S4];                                 // physical row of tile row 64 s + l
+        // ---- a consistent snapshot of the tile -> physical row map: kp chunks are final
+        int prow[S4], kp;
+        for (;;) {
+            const int s1 = lu_ld(sm.seq);
+            if (s1 & 1) { __builtin_amdgcn_s_sleep(1); continue; }
 #pragma unroll
-        for (int s = 0; s < S4; s++) prow[s] = (64 * s + l < N) ? sm.perm[64 * s + l] : 0;
-        const int trow = (t < N) ? sm.perm[t] : 0;    // physical row of tile row t (L fetch)
+            for (int s = 0; s < S4; s++) prow[s] = (64 * s + l < N) ? sm.perm[64 * s + l] : 0;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (lu_ld(sm.seq) == s1) { kp = s1 >> 1; break; }
+        }
+        const int SLO = (CW * kp) >> 6;             // slots below hold pivots of final chunks only
         double acc[S4][CW];
-        // ---- this wave's columns of the block into registers (fused: assembled from K,
-        //      the line terms and the diagonal, row 0 <- 1)
+        // ---- this wave's chunk into registers (fused: assembled from K, the line terms and the
+        //      diagonal, row 0 <- 1)
 #pragma unroll
         for (int s = 0; s < S4; s++) {
             const int r = 64 * s + l, pr = prow[s];
-            const bool okr = r < N && nw > 0;
+            const bool okr = r < N;
             if (!FUSED) {
 #pragma unroll
-                for (int j = 0; j < CW; j++) {
-                    const int d = cw0 + j;
-                    const bool ok = okr && j < nw;
+                for (int jj = 0; jj < CW; jj++) {
+                    const int d = c0 + jj;
+                    const bool ok = okr && jj < nw;
                     double v;
                     if (src.BK) {
                         const double k = ok ? src.BK[(int64_t)pr * N + d] : 0.;
@@ -360,111 +354,93 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                     } else {
                         v = ok ? (src.B ? src.B : A)[(int64_t)pr * N + d] : 0.;
                     }
-                    acc[s][j] = ok ? v : 0.;
+                    acc[s][jj] = ok ? v : 0.;
                 }
             } else {
                 int li[CW];
-                const int64_t o = (int64_t)(okr ? pr : 0) * N + cw0;
+                const int64_t o = (int64_t)(okr ? pr : 0) * N + c0;
                 if ((N & 3) == 0 && nw == CW) {
                     const double2 *k2 = reinterpret_cast<const double2 *>(src.K + o);
                     const int4 *l4 = reinterpret_cast<const int4 *>(src.li + o);
 #pragma unroll
-                    for (int j = 0; j < CW / 2; j++) {
-                        const double2 v = okr ? k2[j] : make_double2(0., 0.);
-                        acc[s][2 * j] = v.x; acc[s][2 * j + 1] = v.y;
+                    for (int jj = 0; jj < CW / 2; jj++) {
+                        const double2 v = okr ? k2[jj] : make_double2(0., 0.);
+                        acc[s][2 * jj] = v.x; acc[s][2 * jj + 1] = v.y;
                     }
 #pragma unroll
-                    for (int j = 0; j < CW / 4; j++) {
-                        const int4 v = okr ? l4[j] : make_int4(-1, -1, -1, -1);
-                        li[4 * j] = v.x; li[4 * j + 1] = v.y; li[4 * j + 2] = v.z; li[4 * j + 3] = v.w;
+                    for (int jj = 0; jj < CW / 4; jj++) {
+                        const int4 v = okr ? l4[jj] : make_int4(-1, -1, -1, -1);
+                        li[4 * jj] = v.x; li[4 * jj + 1] = v.y; li[4 * jj + 2] = v.z; li[4 * jj + 3] = v.w;
                     }
                 } else {
 #pragma unroll
-                    for (int j = 0; j < CW; j++) {
-                        const bool ok = okr && j < nw;
-                        acc[s][j] = ok ? src.K[o + j] : 0.;
-                        li[j] = ok ? src.li[o + j] : -1;
+                    for (int jj = 0; jj < CW; jj++) {
+                        const bool ok = okr && jj < nw;
+                        acc[s][jj] = ok ? src.K[o + jj] : 0.;
+                        li[jj] = ok ? src.li[o + jj] : -1;
                     }
                 }
 #pragma unroll
-                for (int j = 0; j < CW; j++) {
-                    const int d = cw0 + j;
-                    double v = acc[s][j];
-                    if (li[j] >= 0) v = v + src.y[li[j]];
+                for (int jj = 0; jj < CW; jj++) {
+                    const int d = c0 + jj;
+                    double v = acc[s][jj];
+                    if (li[jj] >= 0) v = v + src.y[li[jj]];
                     if (pr == d) v = sm.diag[d < NMAX ? d : 0];
                     if (pr == 0) v = 1.;
-                    acc[s][j] = (okr && j < nw) ? v : 0.;
-                    if (src.dump && okr && j < nw) src.dump[(int64_t)pr * N + d] = v;
+                    acc[s][jj] = (okr && jj < nw) ? v : 0.;
+                    if (src.dump && okr && jj < nw) src.dump[(int64_t)pr * N + d] = v;
                 }
             }
         }
         TACC(PH_BLOAD, tp0);
-        TSTAMP(tr0);
-        // ---- residual rows (physical), columns ascending: wave 0's columns, then wave 1's, ...
+        // ---- residual rows (physical), this chunk's columns in ascending order, chunks in turn
         if (FUSED) {
+            TSTAMP(tr0);
+            lu_wait(sm.rdone, j);
 #pragma unroll
-            for (int wq = 0; wq < NW; wq++) {
-                if (w == wq && nw > 0) {
+            for (int s = 0; s < S4; s++) {
+                const int r = 64 * s + l;
+                if (r < N) {
+                    double sr = sm.resid[prow[s]];
 #pragma unroll
-                    for (int s = 0; s < S4; s++) {
-                        const int r = 64 * s + l;
-                        if (r < N) {
-                            double sr = sm.resid[prow[s]];
-#pragma unroll
-                            for (int j = 0; j < CW; j++) if (j < nw) sr = sr - acc[s][j] * src.pop[cw0 + j];
-                            sm.resid[prow[s]] = sr;
-                        }
-                    }
+                    for (int jj = 0; jj < CW; jj++) if (jj < nw) sr = sr - acc[s][jj] * src.pop[c0 + jj];
+                    sm.resid[prow[s]] = sr;
                 }
-                __syncthreads();
             }
-        } else {
-            __syncthreads();
+            wave_lds_sync();
+            if (l == 0) lu_st(sm.rdone, j + 1);
+            TACC(PH_RSV, tr0);
         }
-        TACC(PH_RSV, tr0);
-        // ---- earlier chunks: L staged by tile row, two barriers a step (prefetching the next
-        //      chunk's rows into registers during this one measured slower)
-        if (c0 > 0) {
-            double pf[CW];
-            for (int kk = 0; kk < c0; kk += CW) {
-                TSTAMP(tf0);
-                lu2_fetch_l(A, N, kk, trow, pf);
-                lu2_stage_l(N, kk, pf, sm);
-                __syncthreads();
-                TACC(PH_T_FETCH, tf0);
-                if (nw > 0) lu2_apply(acc, prow, true, kk, CW, (kk + CW) >> 6, cw0, nw, A, N, sm);
-                TSTAMP(tb0);
-                __syncthreads();
-                TACC(PH_TRSM, tb0);
-            }
+        // ---- the chunks before this one, in order, each once it is published
+        for (int ci = 0; ci < j; ci++) {
+            TSTAMP(tf0);
+            if (ci >= kp) lu_wait(sm.seq, 2 * (ci + 1));
+            TACC(PH_T_FETCH, tf0);
+            const bool earlier = ci < kp;
+            lu_apply(acc, prow, earlier, ci, CW, earlier ? (CW * (ci + 1)) >> 6 : SLO, c0, nw, A, N, sm);
         }
-        // ---- this block's chunks: owner factors, waves to its right apply
+        // ---- this chunk: factor, publish
+        const int nb = nw;
         bool part[S4];
         int lp[S4];
         double rb[S4];
-        for (int wq = 0; wq < NW; wq++) {
-            const int kk = c0 + CW * wq;
-            if (kk >= N) break;
-            const int nb = min(CW, N - kk);
-            TSTAMP(tp1);
-            if (w == wq) lu2_panel(acc, prow, kk, nb, SLO, N, b, part, lp, rb, sm);
-            TACC(PH_PANEL, tp1);
-            TSTAMP(tw0);
-            __syncthreads();                       // the applies of the previous chunk are done
-            if (w == wq) lu2_publish(acc, prow, kk, nb, SLO, A, N, b, part, lp, rb, sm);
-            __syncthreads();
-            TACC(PH_P_WB, tw0);
-            if (w > wq && nw > 0) lu2_apply(acc, prow, false, kk, nb, SLO, cw0, nw, A, N, sm);
-        }
+        TSTAMP(tp1);
+        lu_panel(acc, prow, c0, nb, SLO, N, b, part, lp, rb, sm);
+        TACC(PH_PANEL, tp1);
+        TSTAMP(tw0);
+        if (l == 0) __hip_atomic_store(&sm.seq, 2 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        lu_publish(acc, prow, j, nb, SLO, A, N, b, part, lp, rb, sm);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        wave_lds_sync();
+        if (l == 0) lu_st(sm.seq, 2 * j + 2);
+        TACC(PH_P_WB, tw0);
     }
-    TSTAMP(tw0);
+    TSTAMP(tw1);
     __syncthreads();
-    TACC(PH_BS_WAIT, tw0);
+    TACC(PH_BS_WAIT, tw1);
     back_substitute(A, N, b, sm);
     double emax = 0.;
     if (FUSED && t < N) { const double r = sm.resid[t]; src.df[t] = r; emax = fabs(r); }
     return FUSED ? block_max(emax, sm) : 0.;
 }
-#else
-#include "lvg_lu3.h"
-#endif
