@@ -75,7 +75,7 @@ constexpr int LU_CW = 16;                   // N <= 256 LU: columns per chunk (l
 constexpr int NW   = BT / 64;
 constexpr int NB   = 16;                    // LU panel width (chunk)
 static_assert(NMAX <= BT && BT % 64 == 0 && NMAX % 32 == 0, "at least one row per thread, whole waves");
-constexpr int YCAP = LVG_BIG ? 1 : 2048;    // line terms kept in LDS when 2*nb_lines <= YCAP    // line terms kept in LDS when 2*nb_lines <= YCAP
+constexpr int YCAP = LVG_BIG ? 1 : 2048;    // line terms kept in LDS when 2*nb_lines <= YCAP
 constexpr int TC = 4;                       // columns per thread in the LU register tile (TR rows x TC)
 constexpr int TR = NMAX * 8 / BT;           // tile rows per thread: the BT/8 row groups cover NMAX
 static_assert(TR * (BT / 8) >= NMAX && TR % 2 == 0, "the register tiles cover every row");
