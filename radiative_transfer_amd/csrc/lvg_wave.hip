@@ -293,7 +293,14 @@ __device__ __forceinline__ void wave_line_terms_plain(const LvgDevProblem &P, co
     }
 }
 
-// overlap scheme from the invariants (intensity_single / intensity_pair sequences)
+// overlap scheme from the invariants (intensity_single / intensity_pair sequences).
+// One wave holds every unit at once at the BASELINE sizes, so the lane-divergent paths (single
+// lines, near pairs, far pairs) would run one after the other with their latency chains
+// (record -> grid bisections in LDS -> table fetch) exposed in turn. Instead every lane runs all
+// of them with clamped indices and the results are selected: a single line is a far-only pair
+// with no second line (its own opacity expression, intensity_single), near / far / mixed pairs
+// take the same operations in the same order as intensity_pair. Same values bit for bit; the
+// bisections and table fetches of all paths are in flight together.
 __device__ __forceinline__ void wave_line_terms_overlap(const LvgDevProblem &P, const EscGrids &G,
                                                         const LvgModeLines &M, WaveLayer &sm, const double *inv,
                                                         int cap) {
@@ -304,89 +311,68 @@ __device__ __forceinline__ void wave_line_terms_overlap(const LvgDevProblem &P, 
 #pragma unroll
         for (int i = 0; i < WI_ALL; i++) f[i] = inv[i * cap + q];
         const int n1 = (int)f[WI_N1], n2 = (int)f[WI_N2];
+        const bool pair = n2 >= 0;
+        // a single line's pair fields are not written (wave_line_invariants): indices clamped
+        const int u1 = (int)f[WI_U1], l1 = (int)f[WI_L1];
+        const int u2 = pair ? (int)f[WI_U2] : 0, l2 = pair ? (int)f[WI_L2] : 0;
         const double c0 = f[WI_C], a1 = f[WI_A1], b1 = f[WI_B1];
-        if (n2 < 0) {
-            const double emiss = c0 * a1 * pop[(int)f[WI_U1]];
-            double opac = c0 * b1 * pop[(int)f[WI_L1]] - emiss + MIN_LINE_OPACITY;
-            if (opac < 0.) opac *= INV_TRANS_FACTOR;
-            const double gamma = fabs(sm.vgrad) / (sm.vw * opac);
-            EscIdx ix;
-            ix.k = (int)f[WI_EK];
-            ix.t = f[WI_ET];
-            ov_interval(G.eg, P.esc_ng, gamma, ix.l, ix.u);
-            double tv[4];
-            esc_load(P, ix, tv);
-            const double I = emiss / opac * esc_sum(ix, tv);
-            sm.y[2 * n1] = a1 * (1. + I);
-            sm.y[2 * n1 + 1] = b1 * I;
-            continue;
-        }
-        const int u1 = (int)f[WI_U1], l1 = (int)f[WI_L1], u2 = (int)f[WI_U2], l2 = (int)f[WI_L2];
-        const double a2 = f[WI_A2], b2 = f[WI_B2], dx = f[WI_DX];
+        const double a2 = pair ? f[WI_A2] : 0., b2 = pair ? f[WI_B2] : 0.;
+        const double adx = pair ? fabs(f[WI_DX]) : 2. * max_dx;
         const double em1 = c0 * a1 * pop[u1];
-        double op1 = c0 * (b1 * pop[l1] - a1 * pop[u1]) + MIN_LINE_OPACITY;
+        double op1 = pair ? c0 * (b1 * pop[l1] - a1 * pop[u1]) + MIN_LINE_OPACITY
+                          : c0 * b1 * pop[l1] - em1 + MIN_LINE_OPACITY;
         const double em2 = c0 * a2 * pop[u2];
         double op2 = c0 * (b2 * pop[l2] - a2 * pop[u2]) + MIN_LINE_OPACITY;
         if (op1 < 0.) op1 *= INV_TRANS_FACTOR;
         if (op2 < 0.) op2 *= INV_TRANS_FACTOR;
         const double g1 = fabs(sm.vgrad) / (sm.vw * op1), g2 = fabs(sm.vgrad) / (sm.vw * op2);
-        const bool near = fabs(dx) < max_dx, far = fabs(dx) > max_dx - 0.5;
-        double ep1 = 0., ep2 = 0., ep01 = 0., ep02 = 0., q1 = 0., q2 = 0.;
-        if (near) {
-            OvIdx A, B;
-            A.m = B.m = (int)f[WI_OM];
-            A.y = B.y = f[WI_OY];
-            A.n = (int)f[WI_AN]; A.p = f[WI_AP];
-            B.n = (int)f[WI_BN]; B.p = f[WI_BP];
-            ov_interval(G.og, P.ov_ng, g1, A.l, A.u);
-            ov_interval(G.ogr, P.ov_ngr, g2 / g1, A.k, A.t);
-            ov_interval(G.og, P.ov_ng, g2, B.l, B.u);
-            ov_interval(G.ogr, P.ov_ngr, g1 / g2, B.k, B.t);
-            double v1[16], v2[16], w1[16], w2[16];
-            ov_load(P, P.ov_p1, A, v1);
-            ov_load(P, P.ov_p1, B, v2);
-            ov_load(P, P.ov_p2, A, w1);
-            ov_load(P, P.ov_p2, B, w2);
-            ep1 = ov_sum(A, v1);
-            ep2 = ov_sum(B, v2);
-            q1 = ov_sum(A, w1);
-            q2 = ov_sum(B, w2);
-        }
-        if (far) {
-            EscIdx A, B;
-            A.k = B.k = (int)f[WI_EK];
-            A.t = B.t = f[WI_ET];
-            ov_interval(G.eg, P.esc_ng, g1, A.l, A.u);
-            ov_interval(G.eg, P.esc_ng, g2, B.l, B.u);
-            double v1[4], v2[4];
-            esc_load(P, A, v1);
-            esc_load(P, B, v2);
-            ep01 = esc_sum(A, v1);
-            ep02 = esc_sum(B, v2);
-        }
-        double c = c0;
-        if (fabs(dx) > max_dx) { ep1 = ep01; ep2 = ep02; }
+        const bool near = adx < max_dx, far = adx > max_dx - 0.5;
+        // near: the 4-D overlap tables in both directions
+        OvIdx A, B;
+        A.m = B.m = near ? (int)f[WI_OM] : 0;
+        A.y = B.y = f[WI_OY];
+        A.n = near ? (int)f[WI_AN] : 0; A.p = f[WI_AP];
+        B.n = near ? (int)f[WI_BN] : 0; B.p = f[WI_BP];
+        ov_interval(G.og, P.ov_ng, g1, A.l, A.u);
+        ov_interval(G.ogr, P.ov_ngr, g2 / g1, A.k, A.t);
+        ov_interval(G.og, P.ov_ng, g2, B.l, B.u);
+        ov_interval(G.ogr, P.ov_ngr, g1 / g2, B.k, B.t);
+        // far (and single): the escape table in both directions
+        EscIdx FA, FB;
+        FA.k = FB.k = (int)f[WI_EK];
+        FA.t = FB.t = f[WI_ET];
+        ov_interval(G.eg, P.esc_ng, g1, FA.l, FA.u);
+        ov_interval(G.eg, P.esc_ng, g2, FB.l, FB.u);
+        double v1[16], v2[16], w1[16], w2[16], e1[4], e2[4];
+        ov_load(P, P.ov_p1, A, v1);
+        ov_load(P, P.ov_p1, B, v2);
+        ov_load(P, P.ov_p2, A, w1);
+        ov_load(P, P.ov_p2, B, w2);
+        esc_load(P, FA, e1);
+        esc_load(P, FB, e2);
+        double ep1 = near ? ov_sum(A, v1) : 0., ep2 = near ? ov_sum(B, v2) : 0.;
+        const double q1 = near ? ov_sum(A, w1) : 0., q2 = near ? ov_sum(B, w2) : 0.;
+        const double ep01 = far ? esc_sum(FA, e1) : 0., ep02 = far ? esc_sum(FB, e2) : 0.;
+        const double cm = 2. * (max_dx - adx);
+        if (adx > max_dx) { ep1 = ep01; ep2 = ep02; }
         else if (far) {
-            c = 2. * (max_dx - fabs(dx));
-            ep1 = ep01 * (1. - c) + ep1 * c;
-            ep2 = ep02 * (1. - c) + ep2 * c;
+            ep1 = ep01 * (1. - cm) + ep1 * cm;
+            ep2 = ep02 * (1. - cm) + ep2 * cm;
         }
         double i1 = em1 / op1 * ep1;
         double i2 = em2 / op2 * ep2;
         if (near) {
-            ep1 = q1;
-            ep2 = q2;
-            if (far) {
-                c = 2. * (max_dx - fabs(dx));
-                ep1 *= c; ep2 *= c;
-            }
-            i1 += em2 / op2 * ep1;
-            i2 += em1 / op1 * ep2;
+            double r1 = q1, r2 = q2;
+            if (far) { r1 *= cm; r2 *= cm; }
+            i1 += em2 / op2 * r1;
+            i2 += em1 / op1 * r2;
         }
         sm.y[2 * n1] = a1 * (1. + i1);
         sm.y[2 * n1 + 1] = b1 * i1;
-        sm.y[2 * n2] = a2 * (1. + i2);
-        sm.y[2 * n2 + 1] = b2 * i2;
+        if (pair) {
+            sm.y[2 * n2] = a2 * (1. + i2);
+            sm.y[2 * n2 + 1] = b2 * i2;
+        }
     }
 }
 
