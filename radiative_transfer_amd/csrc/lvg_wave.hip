@@ -307,6 +307,7 @@ __device__ __forceinline__ void wave_line_terms_overlap(const LvgDevProblem &P, 
     const double max_dx = 4.;
     const double *pop = sm.pold;
     for (int q = lane_id(); q < M.nb_units; q += 64) {
+        TSTAMP(lt0);
         double f[WI_ALL];
 #pragma unroll
         for (int i = 0; i < WI_ALL; i++) f[i] = inv[i * cap + q];
@@ -327,6 +328,8 @@ __device__ __forceinline__ void wave_line_terms_overlap(const LvgDevProblem &P, 
         if (op2 < 0.) op2 *= INV_TRANS_FACTOR;
         const double g1 = fabs(sm.vgrad) / (sm.vw * op1), g2 = fabs(sm.vgrad) / (sm.vw * op2);
         const bool near = adx < max_dx, far = adx > max_dx - 0.5;
+        TACC(PH_T_FETCH, lt0);      // timer build: record, populations, opacities, gammas
+        TSTAMP(lt1);
         // near: the 4-D overlap tables in both directions
         OvIdx A, B;
         A.m = B.m = near ? (int)f[WI_OM] : 0;
@@ -343,6 +346,8 @@ __device__ __forceinline__ void wave_line_terms_overlap(const LvgDevProblem &P, 
         FA.t = FB.t = f[WI_ET];
         ov_interval(G.eg, P.esc_ng, g1, FA.l, FA.u);
         ov_interval(G.eg, P.esc_ng, g2, FB.l, FB.u);
+        TACC(PH_T_SOLVE, lt1);      // grid intervals
+        TSTAMP(lt2);
         double v1[16], v2[16], w1[16], w2[16], e1[4], e2[4];
         ov_load(P, P.ov_p1, A, v1);
         ov_load(P, P.ov_p1, B, v2);
@@ -353,6 +358,8 @@ __device__ __forceinline__ void wave_line_terms_overlap(const LvgDevProblem &P, 
         double ep1 = near ? ov_sum(A, v1) : 0., ep2 = near ? ov_sum(B, v2) : 0.;
         const double q1 = near ? ov_sum(A, w1) : 0., q2 = near ? ov_sum(B, w2) : 0.;
         const double ep01 = far ? esc_sum(FA, e1) : 0., ep02 = far ? esc_sum(FB, e2) : 0.;
+        TACC(PH_T_STAGE, lt2);      // table fetch and interpolation sums
+        TSTAMP(lt3);
         const double cm = 2. * (max_dx - adx);
         if (adx > max_dx) { ep1 = ep01; ep2 = ep02; }
         else if (far) {
@@ -373,6 +380,7 @@ __device__ __forceinline__ void wave_line_terms_overlap(const LvgDevProblem &P, 
             sm.y[2 * n2] = a2 * (1. + i2);
             sm.y[2 * n2 + 1] = b2 * i2;
         }
+        TACC(PH_P_RED, lt3);        // intensities and stores
     }
 }
 

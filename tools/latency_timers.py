@@ -42,6 +42,9 @@ print(f"{name}: layer {k} alone, {it} iterations, kernel {ms:.3f} ms = {ms * 1e-
 for i, n in enumerate(names):
     print(f"  {n:16s} {cyc[i] / it:10.0f} cyc/iteration")
 for i, n in [(15, "  (residual hand-off)"), (12, "  (block load)"), (16, "  (L fetch+stage)"), (17, "  (TRSM)"),
-             (21, "  (pre-panel bar+dump)"), (22, "  (bsub diag)"), (23, "  (bsub update)"), (24, "  (wait before bsub)")]:
+             (21, "  (pre-panel bar+dump)"), (22, "  (bsub diag)"), (23, "  (bsub update)"), (24, "  (wait before bsub)")] \
+        if P.mol.nb_lev > 64 else \
+        [(16, "  (lines: record+opacity)"), (17, "  (lines: intervals)"), (18, "  (lines: tables+sums)"),
+         (19, "  (lines: intensities)")]:
     print(f"  {n:22s} {cyc[i] / it:10.0f} cyc/iteration")
 print(f"  sum of phases    {cyc[:9].sum() / it:10.0f} cyc/iteration; raw slots {buf[:32]}")
