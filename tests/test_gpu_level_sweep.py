@@ -47,6 +47,18 @@ def test_wave_level_counts(nlev):
     _run("ph2o45_1024", nlev, 8, "", 1, thin=nlev > 52)
 
 
+# the overlap scheme (OH hyperfine pairs, 4-D table, single lines) on the wave kernel: every lane
+# runs the single / near / far paths with clamped indices (lvg_wave.hip); each NM class up to 40
+# is checked against the oracle (OH-HF level counts are even; at 48 levels the line terms no longer
+# fit the wave kernel's LDS and the block kernel takes the solve)
+WAVE_OV_N = [12, 22, 32, 40]                        # NM = 16, 24, 32, 40
+
+
+@pytest.mark.parametrize("nlev", WAVE_OV_N)
+def test_wave_overlap_level_counts(nlev):
+    _run("oh24_overlap_2048", nlev, 8, "", 1)
+
+
 @pytest.mark.parametrize("nlev", BLOCK_N)
 @pytest.mark.parametrize("wide", [0, 2])
 def test_block_level_counts(nlev, wide):
