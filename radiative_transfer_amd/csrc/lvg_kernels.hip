@@ -79,7 +79,7 @@ constexpr int YCAP = LVG_BIG ? 1 : 2048;    // line terms kept in LDS when 2*nb_
 constexpr int TC = 4;                       // columns per thread in the LU register tile (TR rows x TC)
 constexpr int TR = NMAX * 8 / BT;           // tile rows per thread: the BT/8 row groups cover NMAX
 static_assert(TR * (BT / 8) >= NMAX && TR % 2 == 0, "the register tiles cover every row");
-constexpr int WB = 8 * TC;                  // LU block-column width
+[[maybe_unused]] constexpr int WB = 8 * TC;  // LU block-column width (768-thread kernel)
 #ifndef LVG_COLL_PU
 #define LVG_COLL_PU 4
 #endif
