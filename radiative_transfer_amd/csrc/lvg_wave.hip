@@ -40,6 +40,7 @@ constexpr int WNMAX = LVG_WAVE_NMAX;
 
 struct WaveLayer {                // per-wave LDS
     double pold[WNMAX], pnew[WNMAX], diag[WNMAX];
+    int ivh[6][64];                     // grid interval hints, per lane (ov_interval_hint)
     double y[WYCAP];
     double hist_acc[32];
     double T, Te, vw, vgrad, nmol, ne;
@@ -207,6 +208,23 @@ __device__ __forceinline__ void ov_interval(const double *g, int n, double x, in
     else w = (x - g[j]) / (g[j + 1] - g[j]);
 }
 
+// the same with the lane's previous result h for this lookup (-1: none). On a non-decreasing
+// grid at most one l has g[l] <= x < g[l+1] (or l = n-2 with x = g[n-1]), and locate_index's
+// bisection returns that l, so when h still brackets x it IS the bisection's answer and the
+// bisection is skipped. Converging populations move gamma less and less, so late iterations
+// mostly hit. mono: the grids were checked non-decreasing (solve_wave_kernel) and h is this
+// lane's own record (its first unit); otherwise the plain bisection, h untouched.
+__device__ __forceinline__ void ov_interval_hint(const double *g, int n, double x, int &j, double &w, int &h,
+                                                 bool mono) {
+    const int p = h;
+    const bool hit = mono && p >= 0 && p <= n - 2 && g[p] <= x && (x < g[p + 1] || (p == n - 2 && x == g[n - 1]));
+    j = hit ? p : locate_index(g, n, x);
+    if (mono) h = j;
+    if (j < 0) { j = 0; w = 0.; }
+    else if (j > n - 2) { j = n - 2; w = 1.; }
+    else w = (x - g[j]) / (g[j + 1] - g[j]);
+}
+
 __device__ __forceinline__ void wave_line_invariants(const LvgDevProblem &P, const EscGrids &G, const LvgModeLines &M,
                                                      const WaveLayer &sm, bool ov, double *inv, int cap) {
     for (int q = lane_id(); q < M.nb_units; q += 64) {
@@ -255,7 +273,7 @@ __device__ __forceinline__ void wave_line_invariants(const LvgDevProblem &P, con
 // plain scheme from the invariants: B units per lane per pass, stores last
 __device__ __forceinline__ void wave_line_terms_plain(const LvgDevProblem &P, const EscGrids &G,
                                                       const LvgModeLines &M, WaveLayer &sm, const double *inv,
-                                                      int cap) {
+                                                      int cap, bool mono) {
     const int t = lane_id(), U = M.nb_units;
     constexpr int B = 4;
     for (int q0 = t; q0 < U; q0 += 64 * B) {
@@ -277,7 +295,8 @@ __device__ __forceinline__ void wave_line_terms_plain(const LvgDevProblem &P, co
             const double gamma = fabs(sm.vgrad) / (sm.vw * op[b]);
             ix[b].k = (int)f[b][WI_EK];
             ix[b].t = f[b][WI_ET];
-            ov_interval(G.eg, P.esc_ng, gamma, ix[b].l, ix[b].u);   // esc_func's gamma part
+            // esc_func's gamma part; the lane's first B units keep their intervals as hints
+            ov_interval_hint(G.eg, P.esc_ng, gamma, ix[b].l, ix[b].u, sm.ivh[b][t], mono && q0 < 64);
         }
 #pragma unroll
         for (int b = 0; b < B; b++) esc_load(P, ix[b], tv[b]);
@@ -303,7 +322,7 @@ __device__ __forceinline__ void wave_line_terms_plain(const LvgDevProblem &P, co
 // bisections and table fetches of all paths are in flight together.
 __device__ __forceinline__ void wave_line_terms_overlap(const LvgDevProblem &P, const EscGrids &G,
                                                         const LvgModeLines &M, WaveLayer &sm, const double *inv,
-                                                        int cap) {
+                                                        int cap, bool mono) {
     const double max_dx = 4.;
     const double *pop = sm.pold;
     for (int q = lane_id(); q < M.nb_units; q += 64) {
@@ -336,16 +355,20 @@ __device__ __forceinline__ void wave_line_terms_overlap(const LvgDevProblem &P, 
         A.y = B.y = f[WI_OY];
         A.n = near ? (int)f[WI_AN] : 0; A.p = f[WI_AP];
         B.n = near ? (int)f[WI_BN] : 0; B.p = f[WI_BP];
-        ov_interval(G.og, P.ov_ng, g1, A.l, A.u);
-        ov_interval(G.ogr, P.ov_ngr, g2 / g1, A.k, A.t);
-        ov_interval(G.og, P.ov_ng, g2, B.l, B.u);
-        ov_interval(G.ogr, P.ov_ngr, g1 / g2, B.k, B.t);
+        // the lane's first unit keeps its intervals of the previous iteration as hints
+        const bool hm = mono && q < 64;
+        int (&hint)[6][64] = sm.ivh;
+        const int ln = q & 63;
+        ov_interval_hint(G.og, P.ov_ng, g1, A.l, A.u, hint[0][ln], hm);
+        ov_interval_hint(G.ogr, P.ov_ngr, g2 / g1, A.k, A.t, hint[1][ln], hm);
+        ov_interval_hint(G.og, P.ov_ng, g2, B.l, B.u, hint[2][ln], hm);
+        ov_interval_hint(G.ogr, P.ov_ngr, g1 / g2, B.k, B.t, hint[3][ln], hm);
         // far (and single): the escape table in both directions
         EscIdx FA, FB;
         FA.k = FB.k = (int)f[WI_EK];
         FA.t = FB.t = f[WI_ET];
-        ov_interval(G.eg, P.esc_ng, g1, FA.l, FA.u);
-        ov_interval(G.eg, P.esc_ng, g2, FB.l, FB.u);
+        ov_interval_hint(G.eg, P.esc_ng, g1, FA.l, FA.u, hint[4][ln], hm);
+        ov_interval_hint(G.eg, P.esc_ng, g2, FB.l, FB.u, hint[5][ln], hm);
         TACC(PH_T_SOLVE, lt1);      // grid intervals
         TSTAMP(lt2);
         double v1[16], v2[16], w1[16], w2[16], e1[4], e2[4];
@@ -582,7 +605,7 @@ __device__ __forceinline__ void wave_next_step_post(Ctl &C, Slot &S, int N, Wave
 template <int NM>
 __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const LvgLaunch &Lc, const WaveShared &sh,
                                                  WaveLayer &sm, const EscGrids &G, const int *li, int ldk, double *K,
-                                                 Slot &S, int l, bool from_prev) {
+                                                 Slot &S, int l, bool from_prev, bool mono) {
     const int N = P.N, t = lane_id();
     const LvgModeLines &M = Lc.line_overlap ? P.overlap : P.plain;
     TSTAMP(ts0);
@@ -621,6 +644,8 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
         lrow[j] = (j < N) ? li[row * ldk + jj] : -1;
     }
     if (!boundary) wave_start_pass(C, S, Lc, N, accel ? Lc.max_iter_acc : Lc.max_iter_plain, accel);
+#pragma unroll
+    for (int k = 0; k < 6; k++) sm.ivh[k][t] = -1;   // no interval hints yet for this layer
     for (;;) {
         double a[NM];
         double eq = 0.;
@@ -640,8 +665,8 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
             TACC(PH_CTL, tc0);
             TSTAMP(tl0);
             // line terms y (compute_line_terms)
-            if (Lc.line_overlap) wave_line_terms_overlap(P, G, M, sm, inv, inv_cap);
-            else wave_line_terms_plain(P, G, M, sm, inv, inv_cap);
+            if (Lc.line_overlap) wave_line_terms_overlap(P, G, M, sm, inv, inv_cap, mono);
+            else wave_line_terms_plain(P, G, M, sm, inv, inv_cap, mono);
             wave_sync();
             TACC(PH_LINES, tl0);
             TSTAMP(ta0);
@@ -813,6 +838,14 @@ solve_wave_kernel(const LvgDevProblem *__restrict__ Pp, const LvgLaunch *__restr
         li[r * ldk + d] = M.line_idx[e];
     }
     __syncthreads();
+    // the gamma / gamma-ratio grids non-decreasing (a NaN fails the test): the precondition of
+    // the interval hints (ov_interval_hint)
+    int bad = 0;
+    for (int e = tid; e < o6; e += blockDim.x) {
+        const bool seg = (e >= o1 && e + 1 < o2) || (ov && ((e >= o4 && e + 1 < o5) || (e >= o5 && e + 1 < o6)));
+        if (seg && !(sh.grids[e] <= sh.grids[e + 1])) bad = 1;
+    }
+    const bool mono = __syncthreads_or(bad) == 0;
     const EscGrids G{sh.grids, sh.grids + o1, sh.grids + o2, sh.grids + o3, sh.grids + o4, sh.grids + o5};
     WaveLayer &sm = sh.w[w];
     Slot S = make_slot(P, Lc, blockIdx.x * wpb + w);
@@ -824,12 +857,13 @@ solve_wave_kernel(const LvgDevProblem *__restrict__ Pp, const LvgLaunch *__restr
         if (q >= nq) break;
         const int l = Lc.order ? Lc.order[q] : q;
         if (!Lc.chain_off) {
-            wave_solve_layer<NM>(P, Lc, sh, sm, G, li, ldk, K, S, l, false);
+            wave_solve_layer<NM>(P, Lc, sh, sm, G, li, ldk, K, S, l, false, mono);
         } else {
             // warm chain l, in layer order (one wave per chain)
             const int lo = Lc.chain_off[l], hi = Lc.chain_off[l + 1];
             bool prev = false;
-            for (int k = lo; k < hi; k++) prev = wave_solve_layer<NM>(P, Lc, sh, sm, G, li, ldk, K, S, k, k > lo && prev);
+            for (int k = lo; k < hi; k++)
+                prev = wave_solve_layer<NM>(P, Lc, sh, sm, G, li, ldk, K, S, k, k > lo && prev, mono);
         }
     }
     PH_FLUSH();
