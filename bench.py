@@ -31,8 +31,13 @@ one small RCCL all-reduce of this step's status tensor; the path's only collecti
 Units = calc_new_pop calls (layer-iterations), counted from the per-layer status.
 
 Inputs (layer SoA) are resident in HBM before the timed region; `value` never includes
-PCIe. The host entry (lvg_solve_layers: layer upload + populations both ways) is timed
-once after the timed region and reported as `host_entry_value`.
+PCIe (the task's measurement contract). The host entry (lvg_solve_layers:
+layer upload + populations both ways) is timed over the same --steps after the timed region
+and reported beside it as `host_entry_value` / `host_entry`.
+
+CPU baseline (rank 0, N = 1): SURVEY 8(d)'s -O3 -march=native -fopenmp build of the oracle
+(reference arithmetic, contraction allowed, compiled on this host) on the job's CPU share and
+on one thread, and the bit-exact checker build on the job's share, each on a bounded sample.
 
 Prints ONE JSON line on rank 0.
 """
@@ -182,11 +187,13 @@ class Provenance:
 
 # ---- CPU baseline (the oracle: test infrastructure, timed beside the GPU) ---------------
 
-def cpu_leg(prob, layers, opts, budget_s: float, threads: int, chain_len: int = 0):
+def cpu_leg(prob, layers, opts, budget_s: float, threads: int, chain_len: int = 0, ref=False):
     """Oracle (C restatement, OpenMP schedule(dynamic,1) over layers, or over clouds for
-    warm chains as the reference's shock-model loop) on a bounded sample."""
+    warm chains as the reference's shock-model loop) on a bounded sample. ref="native":
+    the timing build (reference arithmetic, -O3 -march=native -fopenmp, contraction
+    allowed); ref=False: the bit-exact checker build."""
     from oracle import oracle
-    oracle.build()
+    oracle.lib(ref)
     done = its = 0
     chunk = max(8, 4 * threads)
     if chain_len:
@@ -196,9 +203,9 @@ def cpu_leg(prob, layers, opts, budget_s: float, threads: int, chain_len: int = 
         idx = np.arange(done, min(done + chunk, layers.nb_lay))
         sub = layers.subset(idx)
         if chain_len:
-            _, st = oracle.solve_chains(prob, sub, chain_offsets(idx.size, chain_len), opts, nthreads=threads)
+            _, st = oracle.solve_chains(prob, sub, chain_offsets(idx.size, chain_len), opts, nthreads=threads, ref=ref)
         else:
-            _, st = oracle.solve_layers(prob, sub, opts, nthreads=threads)
+            _, st = oracle.solve_layers(prob, sub, opts, nthreads=threads, ref=ref)
         its += int(st["iterations"].sum())
         done += idx.size
     dt = time.perf_counter() - t0
@@ -211,16 +218,26 @@ def chain_offsets(n: int, chain_len: int) -> np.ndarray:
 
 
 def cpu_baseline(prob, layers, opts, budget_s: float, chain_len: int = 0):
+    """SURVEY 8(d)'s CPU baseline: the oracle's reference-arithmetic build compiled -O3
+    -march=native -fopenmp on this host (contraction allowed; a timing leg, not a checker),
+    on the job's CPU share; beside it the same build on one thread and the bit-exact checker
+    build (-O3 -march=x86-64-v3 -ffp-contract=off) on the job's share."""
+    from oracle import oracle
     info = host_info()
     # all the CPUs this process may use; the GPU box caps a job's share (OMP_NUM_THREADS)
     threads = info["affinity_cpus"]
     if info["omp_num_threads"] and info["omp_num_threads"].isdigit():
         threads = min(threads, int(info["omp_num_threads"]))
-    v_all, s_all = cpu_leg(prob, layers, opts, budget_s, threads, chain_len)
-    v_one, s_one = cpu_leg(prob, layers, opts, budget_s, 1, chain_len)
+    v_all, s_all = cpu_leg(prob, layers, opts, budget_s, threads, chain_len, ref="native")
+    v_one, s_one = cpu_leg(prob, layers, opts, budget_s, 1, chain_len, ref="native")
+    v_chk, s_chk = cpu_leg(prob, layers, opts, budget_s, threads, chain_len, ref=False)
+    sched = "OpenMP schedule(dynamic,1) over " + ("clouds" if chain_len else "layers")
     return {"value": v_all, "unit": UNIT, "cores": threads, "kind": "port",
-            "sample": f"{s_all}, oracle/lvg_oracle.c -O3 OpenMP schedule(dynamic,1), {threads} threads",
-            "one_thread": {"value": v_one, "unit": UNIT, "cores": 1, "sample": s_one},
+            "sample": f"{s_all}; oracle/lvg_oracle.c {oracle.NATIVE_FLAGS}, {sched}, {threads} threads",
+            "flags": oracle.NATIVE_FLAGS,
+            "one_thread": {"value": v_one, "unit": UNIT, "cores": 1, "sample": s_one, "flags": oracle.NATIVE_FLAGS},
+            "checker_build": {"value": v_chk, "unit": UNIT, "cores": threads, "sample": s_chk,
+                              "flags": "-O3 -march=x86-64-v3 -fopenmp -ffp-contract=off (bit-exact checker)"},
             "host": info}
 
 
@@ -445,12 +462,20 @@ def run_rank(args) -> int:
 
     host_value = None
     if rank == 0 and world == 1 and not args.no_host_entry and not stub:
+        # the host entry (lvg_solve_layers: layer upload, populations both ways over PCIe),
+        # timed over the same --steps after the device-resident region
+        its_h = 0
         th = time.perf_counter()
-        if offs is not None:
-            _, sh = solver.solve_chains(mine, offs, opts)
-        else:
-            _, sh = solver.solve_layers(mine, opts)
-        host_value = int(sh["iterations"].sum()) / (time.perf_counter() - th)
+        for _ in range(args.steps):
+            if offs is not None:
+                _, sh = solver.solve_chains(mine, offs, opts)
+            else:
+                _, sh = solver.solve_layers(mine, opts)
+            its_h += int(sh["iterations"].sum())
+        dth = time.perf_counter() - th
+        host_value = {"value": its_h / dth, "unit": UNIT, "steps": args.steps, "ms_per_step": 1e3 * dth / args.steps,
+                      "entry": "lvg_solve_chains" if offs is not None else "lvg_solve_layers",
+                      "note": "host buffers in and out (PCIe included); value is the device entry on HBM-resident buffers"}
 
     if rank == 0:
         print(json.dumps(report(args, world, N, total, L_cfg, lo, hi, units_total, units_local, nonconv, max_rel,
@@ -542,7 +567,8 @@ def report(args, world, N, total, L_cfg, lo, hi, units_total, units_local, nonco
         "provenance": prov_rec,
     }
     if host_value is not None:
-        out["host_entry_value"] = host_value
+        out["host_entry_value"] = host_value["value"]
+        out["host_entry"] = host_value
     if world == 1 and not args.no_cpu and not stub:
         out["cpu_baseline"] = cpu_baseline(prob, mine, opts, args.cpu_budget, args.chain_len)
     return out

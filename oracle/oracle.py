@@ -25,6 +25,32 @@ REF_LIB = {0: LIB_PATH, 7: os.path.join(HERE, "_build", "liblvg_oracle_ref.so"),
            4: os.path.join(HERE, "_build", "liblvg_oracle_ref_pow.so")}
 REF_LIB_PATH = REF_LIB[7]
 _libs = {}
+# the CPU timing leg (bench.py cpu_baseline): reference arithmetic, -O3 -march=native -fopenmp,
+# contraction allowed; built per host CPU model, since -march=native code must not move
+NATIVE_FLAGS = "-O3 -march=native -fopenmp -DORACLE_REF_ARITH (fp contraction allowed)"
+
+
+def _cpu_tag() -> str:
+    import hashlib
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith(("model name", "flags")):
+                    model += line
+    except OSError:
+        pass
+    return hashlib.sha1(model.encode()).hexdigest()[:12]
+
+
+def native_lib_path() -> str:
+    return os.path.join(HERE, "_build", "native", _cpu_tag(), "liblvg_oracle_native.so")
+
+
+def build_native() -> str:
+    p = native_lib_path()
+    subprocess.check_call(["make", "-s", "-C", HERE, "native", f"NATIVE_OUT={os.path.dirname(p)}"])
+    return p
 
 
 def _stale() -> bool:
@@ -44,11 +70,16 @@ def build(force: bool = False) -> str:
 
 def lib(ref=False):
     """The bit-exact oracle, or with ref=True its reference-arithmetic build; ref="exp",
-    "lu" or "pow" undoes that one choice only."""
-    mask = REF_MASK[ref]
-    if mask not in _libs:
-        build()
-        L = C.CDLL(REF_LIB[mask])
+    "lu" or "pow" undoes that one choice only; ref="native" is the CPU timing leg's build
+    (reference arithmetic, -march=native, contraction allowed: not a checker)."""
+    key = ref if ref == "native" else REF_MASK[ref]
+    mask = 7 if ref == "native" else key
+    if key not in _libs:
+        if ref == "native":
+            L = C.CDLL(build_native())
+        else:
+            build()
+            L = C.CDLL(REF_LIB[mask])
         d, i, vp = C.c_double, C.c_int, C.c_void_p
         dp = C.POINTER(C.c_double)
         L.oracle_solve_layers.argtypes = [vp, vp, dp, vp, vp, i]
@@ -74,8 +105,8 @@ def lib(ref=False):
         L.oracle_log10.restype = d
         L.oracle_ref_arith.restype = i
         assert L.oracle_ref_arith() == mask
-        _libs[mask] = L
-    return _libs[mask]
+        _libs[key] = L
+    return _libs[key]
 
 
 def _nz(a):

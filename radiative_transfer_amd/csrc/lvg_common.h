@@ -25,13 +25,13 @@ __device__ unsigned long long lvg_phase_cycles[32];
 // sums kept in LDS (no global atomics inside the timed code: queued atomics would hold
 // up the vmcnt waits of later loads), flushed once per block
 __shared__ unsigned long long lvg_ph_lds[32];
-#define RACC(ph, v0) do { if (threadIdx.x == 0) { unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); \
+#define RACC(ph, v0) do { if (lvg_tid() == 0) { unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); \
     lvg_ph_lds[ph] += t_ - (v0); } } while (0)
-#define TACC(ph, v0) do { if (threadIdx.x == 0) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+#define TACC(ph, v0) do { if (lvg_tid() == 0) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
     lvg_ph_lds[ph] += t_ - (v0); } } while (0)
-#define PH_INIT() do { if (threadIdx.x < 32) lvg_ph_lds[threadIdx.x] = 0; __syncthreads(); } while (0)
-#define PH_FLUSH() do { __syncthreads(); if (threadIdx.x < 32 && lvg_ph_lds[threadIdx.x]) \
-    atomicAdd(&lvg_phase_cycles[threadIdx.x], lvg_ph_lds[threadIdx.x]); } while (0)
+#define PH_INIT() do { if (lvg_tid() < 32) lvg_ph_lds[lvg_tid()] = 0; __syncthreads(); } while (0)
+#define PH_FLUSH() do { __syncthreads(); if (lvg_tid() < 32 && lvg_ph_lds[lvg_tid()]) \
+    atomicAdd(&lvg_phase_cycles[lvg_tid()], lvg_ph_lds[lvg_tid()]); } while (0)
 #else
 #define TSTAMP(v) do {} while (0)
 #define TACC(ph, v0) do {} while (0)
@@ -42,6 +42,17 @@ __shared__ unsigned long long lvg_ph_lds[32];
 #endif
 
 constexpr int NHIST = LVG_HIST_SLOTS;
+
+// The thread index behind an empty asm, so that nothing derived from it (per-thread row
+// addresses of the slot arrays, LDS offsets, lane masks) is hoisted out of the persistent
+// loops and kept live across the LU: in the block kernels those hoisted values were what
+// pushed solve_kernel into scratch (128 VGPRs spilled, 280 B/lane, round 4). Recomputing
+// them where they are used costs a few integer instructions per use.
+__device__ __forceinline__ int lvg_tid() {
+    int v = threadIdx.x;
+    __asm__ volatile("" : "+v"(v));
+    return v;
+}
 
 constexpr double BOLTZMANN_CONSTANT    = 1.380649e-16;
 constexpr double CM_INVERSE_TO_KELVINS = 1.438776877;
@@ -238,11 +249,11 @@ __device__ __forceinline__ void layer_scalars(const LvgDevProblem &P, const LvgL
 // the compiled molecule rule, copied to LDS once per launch (BTH threads)
 template <int BTH, class SM>
 __device__ __forceinline__ void load_rule_table(const LvgDevProblem &P, SM &sm) {
-    for (int e = threadIdx.x; e < LVG_MAX_CLASSES * LVG_MAX_TERMS; e += BTH) {
+    for (int e = lvg_tid(); e < LVG_MAX_CLASSES * LVG_MAX_TERMS; e += BTH) {
         (&sm.ttab[0][0])[e] = (&P.terms.table[0][0])[e];
         (&sm.tcombo[0][0])[e] = (&P.terms.combo[0][0])[e];
     }
-    for (int e = threadIdx.x; e < LVG_MAX_CLASSES; e += BTH) {
+    for (int e = lvg_tid(); e < LVG_MAX_CLASSES; e += BTH) {
         sm.tet[e] = P.terms.etable[e];
         sm.tgrp[e] = P.terms.group[e];
     }
@@ -264,7 +275,7 @@ __device__ __forceinline__ void load_rule_table(const LvgDevProblem &P, SM &sm) 
 template <int BTH, int PU, class SM>
 __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P, SM &sm, double *K, double *B,
                                                           uint8_t *cls_lds, bool electrons = true) {
-    const int N = P.N, t = threadIdx.x;
+    const int N = P.N, t = lvg_tid();
     const double T = sm.T, Te = sm.Te;
     const int nt = (N + 15) >> 4, ntiles = nt * (nt + 1) / 2;
     const int fl = (t >> 4) & 15, sl = t & 15;

@@ -58,7 +58,7 @@ namespace LVG_NS {
 // timer build of the 256-thread kernel: lane 0 of every wave accumulates (LDS atomics), so
 // the phases of waves that work while wave 0 waits are counted too (sums over 4 waves)
 #undef TACC
-#define TACC(ph, v0) do { if ((threadIdx.x & 63) == 0) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+#define TACC(ph, v0) do { if ((lvg_tid() & 63) == 0) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
     atomicAdd(&lvg_ph_lds[ph], t_ - (v0)); } } while (0)
 #endif
 
@@ -84,6 +84,13 @@ static_assert(TR * (BT / 8) >= NMAX && TR % 2 == 0, "the register tiles cover ev
 #define LVG_COLL_PU 4
 #endif
 constexpr int COLL_PU = LVG_COLL_PU;        // 16x16 pair tiles per batch of the in-kernel collision build
+
+// The driver state of solve_layer (iteration control, pass flags) goes through LDS around
+// each LU, so that none of it occupies registers while the LU runs.
+struct Drv {
+    Ctl C;
+    int boundary, iters, retry;
+};
 
 #if LVG_BIG
 struct Smem {
@@ -138,10 +145,11 @@ struct Smem {
     int8_t tet[LVG_MAX_CLASSES], tgrp[LVG_MAX_CLASSES];
     double dust[LVG_MAX_DUST];
     int    layer, pidx;
+    Drv    drv;                 // solve_layer's driver state across the LU
 };
 
 __device__ __forceinline__ double block_max(double v, Smem &sm) {
-    const int t = threadIdx.x, w = t >> 6;
+    const int t = lvg_tid(), w = t >> 6;
     v = wave_max(v);
     __syncthreads();
     if ((t & 63) == 0) sm.red[w] = v;
@@ -153,7 +161,7 @@ __device__ __forceinline__ double block_max(double v, Smem &sm) {
 }
 
 __device__ __forceinline__ void layer_setup(const LvgDevProblem &P, const LvgLaunch &Lc, int l, Smem &sm) {
-    if (threadIdx.x == 0) layer_scalars(P, Lc, l, sm);
+    if (lvg_tid() == 0) layer_scalars(P, Lc, l, sm);
     __syncthreads();
 }
 
@@ -170,7 +178,7 @@ __device__ __forceinline__ void layer_collisions(const LvgDevProblem &P, Smem &s
 __device__ __forceinline__ void compute_line_terms(const LvgDevProblem &P, const LvgModeLines &M, const Smem &sm,
                                                    const double *pop, double *y) {
     const EscGrids G = global_grids(P);
-    for (int q = threadIdx.x; q < M.nb_units; q += BT) {
+    for (int q = lvg_tid(); q < M.nb_units; q += BT) {
         int n1 = M.unit_l0[q], n2 = M.unit_l1[q];
         if (n2 < 0) {
             double I = intensity_single(P, G, M, sm, n1, pop);
@@ -194,7 +202,7 @@ __device__ __forceinline__ void compute_line_terms(const LvgDevProblem &P, const
 // are formed where the LU loads them (block_lu_solve, fused).
 __device__ __forceinline__ void column_diagonals(const LvgDevProblem &P, const LvgModeLines &M,
                                                  const double *K, const double *y, Smem &sm) {
-    const int N = P.N, t = threadIdx.x;
+    const int N = P.N, t = lvg_tid();
     for (int d = t; d < N; d += BT) {
         double a = 0.;
         for (int r0 = 0; r0 < N; r0 += 16) {
@@ -243,7 +251,7 @@ struct LuSrc {
 //      rows above; every entry receives its updates for k descending (oracle order).
 //      b: LDS [N] by physical row; on return sm.blog holds x (logical = level order).
 __device__ __forceinline__ void back_substitute(const double *A, int N, const double *b, Smem &sm) {
-    const int t = threadIdx.x;
+    const int t = lvg_tid();
     TSTAMP(tb0);
     for (int i = t; i < N; i += BT) sm.blog[i] = b[sm.perm[i]];
     __syncthreads();
@@ -344,7 +352,7 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
     // rows with pos[p] >= kk take part. One row per thread (N <= NMAX = BT), the row's
     // right-hand side b[p] in a register; the pivot candidate of each wave publishes
     // its row and its b through LDS.
-    const int t = threadIdx.x, w = t >> 6;
+    const int t = lvg_tid(), w = t >> 6;
     double rw[NB];
     const bool valid = t < N;
     const int p = valid ? t : 0;
@@ -460,8 +468,8 @@ __device__ __forceinline__ void panel_factor(double *A, int N, int kk, int nb, d
 template <int R>
 __device__ __forceinline__ void panel_factor_wave(double *A, int N, int kk, int nb, double *b, Smem &sm, int w0,
                                                   const int (&rows)[R]) {
-    if ((__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6) == w0) {
-        const int ln = threadIdx.x & 63;
+    if ((__builtin_amdgcn_readfirstlane(lvg_tid()) >> 6) == w0) {
+        const int ln = lvg_tid() & 63;
         double rw[R][NB], rb[R];
         bool act[R], part[R];
         int lp[R];
@@ -553,7 +561,7 @@ __device__ __forceinline__ void panel_factor_wave(double *A, int N, int kk, int 
 }
 
 __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Smem &sm, const LuSrc &src, const bool FUSED) {
-    const int t = threadIdx.x;
+    const int t = lvg_tid();
     const int rg = t >> 3, cg = t & 7;   // tile rows TR*rg.., columns TC*cg..
     double s_acc = (t == 0) ? 1. : 0.;             // residual row t (FUSED)
     for (int i = t; i < N; i += BT) { sm.perm[i] = i; sm.pos[i] = i; }
@@ -841,7 +849,7 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
 // sums runs in one thread in the reference's k order; the small system is solved
 // by thread 0 exactly as oracle_lu_solve does.
 __device__ __forceinline__ void accel_step(Ctl &C, Slot &S, int N, Smem &sm) {
-    const int t = threadIdx.x;
+    const int t = lvg_tid();
     const int np = C.nb_prev - 1;
     const double *r0 = ring(S.res, C.hr, 0, N);
     const double *p0 = ring(S.prev, C.hp, 0, N);
@@ -874,7 +882,7 @@ __device__ __forceinline__ void accel_step(Ctl &C, Slot &S, int N, Smem &sm) {
 // iteration_control::next_step (iteration_control.h:84-137), split around the
 // calc_new_pop solve so that the layer driver has a single LU call site.
 __device__ __forceinline__ void next_step_pre(Ctl &C, const LvgDevProblem &P, Slot &S, Smem &sm) {
-    const int N = P.N, t = threadIdx.x;
+    const int N = P.N, t = lvg_tid();
     // prev_level_pop.push_front(pop_old)
     C.hp = (C.hp + NHIST - 1) & (NHIST - 1);
     C.np++;
@@ -888,7 +896,7 @@ __device__ __forceinline__ void next_step_pre(Ctl &C, const LvgDevProblem &P, Sl
 }
 
 __device__ __forceinline__ void next_step_post(Ctl &C, const LvgDevProblem &P, Slot &S, Smem &sm, double eq) {
-    const int N = P.N, t = threadIdx.x;
+    const int N = P.N, t = lvg_tid();
     C.eq_error = eq;
     if (C.acceleration && C.iter_nb >= C.accel_start) C.nb_after_accel++;
     const bool better = C.eq_error < C.best_eq;
@@ -935,7 +943,7 @@ __device__ __forceinline__ void start_pass(Ctl &C, const LvgDevProblem &P, Slot 
     C.eq_error = C.pop_error = C.rel_error = 0.;
     C.hp = C.hr = 0;
     C.np = C.nr = 0;
-    for (int i = threadIdx.x; i < N; i += BT) S.opt[i] = 0.;
+    for (int i = lvg_tid(); i < N; i += BT) S.opt[i] = 0.;
     __syncthreads();
 }
 
@@ -943,7 +951,7 @@ __device__ __forceinline__ void start_pass(Ctl &C, const LvgDevProblem &P, Slot 
 // warm chain and the previous layer of the chain converged (:247-249). Returns is_found.
 __device__ __forceinline__ bool solve_layer(const LvgDevProblem &P, const LvgLaunch &Lc, int l, Slot &S, Smem &sm,
                                             bool from_prev) {
-    const int N = P.N, t = threadIdx.x;
+    const int N = P.N, t = lvg_tid();
     const LvgModeLines &M = Lc.line_overlap ? P.overlap : P.plain;
     TSTAMP(ts0);
     RSTAMP(rs0);
@@ -1003,8 +1011,14 @@ __device__ __forceinline__ bool solve_layer(const LvgDevProblem &P, const LvgLau
             if (Bdg) { src.BK = Kl; src.BE = P.einst; src.BD = Bdg; }
         }
         for (int i = t; i < N; i += BT) sm.bvec[i] = (i == 0) ? 1. : 0.;
+        if (t == 0) { sm.drv.C = C; sm.drv.boundary = boundary; sm.drv.iters = iters; sm.drv.retry = retry; }
         __syncthreads();
         const double eq = block_lu_solve(S.A, N, sm.bvec, sm, src, !boundary);
+        __asm__ volatile("" ::: "memory");       // reload the driver state (no register copy across the LU)
+        C = sm.drv.C;
+        boundary = sm.drv.boundary;
+        iters = sm.drv.iters;
+        retry = sm.drv.retry;
         if (boundary) {
             TACC(PH_BOUNDARY, tb0);
             for (int i = t; i < N; i += BT) { sm.pold[i] = sm.blog[i]; S.given[i] = sm.blog[i]; }
@@ -1059,8 +1073,36 @@ __global__ void __launch_bounds__(BT, OCC) solve_kernel(const LvgDevProblem *__r
     load_rule_table<BT>(P, sm);
     Slot S = make_slot(P, Lc, blockIdx.x);
     const int nq = Lc.chain_off ? Lc.nb_chain : Lc.nb_lay;
+#if !LVG_BIG
+    // one solve_layer call site (one copy of the LU code): an independent layer is a chain
+    // of one layer; k runs over the current queue item's layers [k, hi)
+    int k = 0, hi = 0;
+    bool prev = false;
     for (;;) {
-        if (threadIdx.x == 0) {
+        if (k >= hi) {
+            if (lvg_tid() == 0) {
+                const int q = atomicAdd(Lc.counter, 1);
+                sm.layer = (q < nq && Lc.order) ? Lc.order[q] : q;
+                sm.pidx = q;
+            }
+            __syncthreads();
+            const int item = sm.layer, q = sm.pidx;
+            __syncthreads();
+            if (q >= nq) break;
+            // warm chain: layers in order, each from its predecessor if that converged
+            k = Lc.chain_off ? Lc.chain_off[item] : item;
+            hi = Lc.chain_off ? Lc.chain_off[item + 1] : item + 1;
+            prev = false;
+            continue;
+        }
+        prev = solve_layer(P, Lc, k, S, sm, prev);
+        k++;
+    }
+#else
+    // 768-thread kernel: two call sites allocate better at its 168-register budget (725 vs
+    // 3.7 K VGPRs spilled with the single call site)
+    for (;;) {
+        if (lvg_tid() == 0) {
             const int q = atomicAdd(Lc.counter, 1);
             sm.layer = (q < nq && Lc.order) ? Lc.order[q] : q;
             sm.pidx = q;
@@ -1078,6 +1120,7 @@ __global__ void __launch_bounds__(BT, OCC) solve_kernel(const LvgDevProblem *__r
             for (int k = lo; k < hi; k++) prev = solve_layer(P, Lc, k, S, sm, k > lo && prev);
         }
     }
+#endif
     PH_FLUSH();
 }
 
@@ -1089,7 +1132,7 @@ __global__ void __launch_bounds__(BT, OCC) debug_kernel(const LvgDevProblem *__r
     const LvgLaunch &Lc = *Lp;
     load_rule_table<BT>(P, sm);
     Slot S = make_slot(P, Lc, 0);
-    const int N = P.N, t = threadIdx.x;
+    const int N = P.N, t = lvg_tid();
     const LvgModeLines &M = Lc.line_overlap ? P.overlap : P.plain;
     layer_setup(P, Lc, 0, sm);
     layer_collisions(P, sm, S.K, nullptr);
@@ -1124,7 +1167,7 @@ __global__ void __launch_bounds__(BT, OCC) lum_kernel(const LvgDevProblem *__res
     load_rule_table<BT>(P, sm);
     Slot S = make_slot(P, Lc, blockIdx.x);
     const LvgModeLines &M = P.plain;
-    const int N = P.N, t = threadIdx.x, T = A.nb_trans, nl = Lc.nb_lay;
+    const int N = P.N, t = lvg_tid(), T = A.nb_trans, nl = Lc.nb_lay;
     const int64_t ld = Lc.soa_ld;
     for (;;) {
         if (t == 0) sm.layer = atomicAdd(Lc.counter, 1);
@@ -1182,7 +1225,7 @@ __global__ void __launch_bounds__(BT, OCC) lum_kernel(const LvgDevProblem *__res
 // cloud average of the luminosity, summed in layer order (one thread per transition)
 __global__ void __launch_bounds__(64) lum_reduce_kernel(const LvgLumArgs *__restrict__ Ap, int nl) {
     const LvgLumArgs &A = *Ap;
-    const int tr = blockIdx.x * blockDim.x + threadIdx.x;
+    const int tr = blockIdx.x * blockDim.x + lvg_tid();
     if (tr >= A.nb_trans) return;
     double s = 0.;
     for (int l = 0; l < nl; l++) s += A.lum_arr[(int64_t)tr * nl + l] * A.dz[l];
@@ -1228,7 +1271,7 @@ __global__ void __launch_bounds__(BT, COLL_K_OCC) coll_kernel(const LvgDevProble
     const int rb = (G % 8 == 0) ? (b % 8) * (G / 8) + b / 8 : b;
     for (int pos = rb; pos < Lc.nb_lay; pos += G) {
         const int l = Lc.coll_order ? Lc.coll_order[pos] : pos;
-        if (threadIdx.x == 0) layer_scalars(P, Lc, l, sm);
+        if (lvg_tid() == 0) layer_scalars(P, Lc, l, sm);
         __syncthreads();
         double *Kl = const_cast<double *>(Lc.kall) + l * NN;
         build_collision_operators<BT, COLL_K_PU>(P, sm, Kl, Lc.ball ? const_cast<double *>(Lc.ball) + l * NN : nullptr,
@@ -1237,7 +1280,7 @@ __global__ void __launch_bounds__(BT, COLL_K_OCC) coll_kernel(const LvgDevProble
             // B's diagonal only (no electron rates: B = K + A/2 above the diagonal, K below):
             // minus the ascending column sum, as build_collision_operators forms it
             const int N = P.N;
-            for (int d = threadIdx.x; d < N; d += BT) {
+            for (int d = lvg_tid(); d < N; d += BT) {
                 double a = 0.;
                 for (int r = 0; r < N; r++) {
                     if (r == d) continue;

@@ -54,7 +54,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 __device__ __forceinline__ void lu_panel(double (&acc)[S4][CW], const int (&prow)[S4], int kk, int nb, int s_lo,
                                          int N, const double *b, bool (&part)[S4], int (&lp)[S4],
                                          double (&rb)[S4], Smem &sm) {
-    const int ln = threadIdx.x & 63;
+    const int ln = lvg_tid() & 63;
     bool act[S4];
 #pragma unroll
     for (int s = 0; s < S4; s++) {
@@ -174,7 +174,7 @@ __device__ __forceinline__ void lu_wait(const int &x, int v) {
 // are pivots of earlier chunks).
 __device__ __forceinline__ void lu_apply(double (&acc)[S4][CW], const int (&prow)[S4], bool earlier, int ci, int nb,
                                          int s_up, int cw0, int nw, double *A, int N, Smem &sm) {
-    const int l = threadIdx.x & 63, w = threadIdx.x >> 6, kk = ci * CW;
+    const int l = lvg_tid() & 63, w = lvg_tid() >> 6, kk = ci * CW;
     double (*Ub)[CW] = sm.Ub[w];
     TSTAMP(ta0);
     // the chunk's pivot rows in this wave's columns to Ub (their owner lanes)
@@ -225,12 +225,12 @@ __device__ __forceinline__ void lu_apply(double (&acc)[S4][CW], const int (&prow
     TSTAMP(tg0);
     // rows taking the update: below the chunk's pivots (logical position >= kk + nb)
     bool take[S4];
-    const double *lsrc[S4];
+    unsigned loff[S4];                            // 32-bit offsets of the L rows from A
 #pragma unroll
     for (int s = 0; s < S4; s++) {
         const int r = 64 * s + l;
         take[s] = s >= s_up && r < N && (earlier ? r : sm.pos[prow[s]]) >= kk + nb;
-        lsrc[s] = A + (int64_t)(take[s] ? prow[s] : 0) * N + kk;
+        loff[s] = (unsigned)((take[s] ? prow[s] : 0) * N + kk);
     }
     constexpr int MG = 4;                         // columns of L per load group
 #pragma unroll
@@ -241,7 +241,7 @@ __device__ __forceinline__ void lu_apply(double (&acc)[S4][CW], const int (&prow
             for (int s = 0; s < S4; s++) {
                 if (s >= s_up) {
                     if ((N & 1) == 0) {
-                        const double2 *p2 = reinterpret_cast<const double2 *>(lsrc[s] + g);
+                        const double2 *p2 = reinterpret_cast<const double2 *>(A + loff[s] + g);
 #pragma unroll
                         for (int h = 0; h < MG / 2; h++) {
                             const double2 v = take[s] ? p2[h] : make_double2(0., 0.);
@@ -249,7 +249,7 @@ __device__ __forceinline__ void lu_apply(double (&acc)[S4][CW], const int (&prow
                         }
                     } else {
 #pragma unroll
-                        for (int h = 0; h < MG; h++) a[s][h] = take[s] ? lsrc[s][g + h] : 0.;
+                        for (int h = 0; h < MG; h++) a[s][h] = take[s] ? A[loff[s] + g + h] : 0.;
                     }
                 }
             }
@@ -257,15 +257,19 @@ __device__ __forceinline__ void lu_apply(double (&acc)[S4][CW], const int (&prow
             for (int mm = 0; mm < MG; mm++) {
                 const int m = g + mm;
                 if (m < nb) {
-                    double u[CW];
-                    const double2 *up = reinterpret_cast<const double2 *>(&Ub[m][0]);
+                    // U row m in two halves of 8 (16 registers live instead of 32)
 #pragma unroll
-                    for (int j = 0; j < CW / 2; j++) { const double2 v = up[j]; u[2 * j] = v.x; u[2 * j + 1] = v.y; }
+                    for (int hh = 0; hh < CW; hh += CW / 2) {
+                        double u[CW / 2];
+                        const double2 *up = reinterpret_cast<const double2 *>(&Ub[m][hh]);
 #pragma unroll
-                    for (int s = 0; s < S4; s++) {
-                        if (s >= s_up) {
+                        for (int j = 0; j < CW / 4; j++) { const double2 v = up[j]; u[2 * j] = v.x; u[2 * j + 1] = v.y; }
 #pragma unroll
-                            for (int c = 0; c < CW; c++) acc[s][c] = fma(-a[s][mm], u[c], acc[s][c]);
+                        for (int s = 0; s < S4; s++) {
+                            if (s >= s_up) {
+#pragma unroll
+                                for (int c = 0; c < CW / 2; c++) acc[s][hh + c] = fma(-a[s][mm], u[c], acc[s][hh + c]);
+                            }
                         }
                     }
                 }
@@ -280,7 +284,7 @@ __device__ __forceinline__ void lu_apply(double (&acc)[S4][CW], const int (&prow
 __device__ __forceinline__ void lu_publish(const double (&acc)[S4][CW], const int (&prow)[S4], int ci, int nb,
                                             int s_lo, double *A, int N, double *b, const bool (&part)[S4],
                                             const int (&lp)[S4], const double (&rb)[S4], Smem &sm) {
-    const int ln = threadIdx.x & 63, kk = ci * CW;
+    const int ln = lvg_tid() & 63, kk = ci * CW;
 #pragma unroll
     for (int s = 0; s < S4; s++) {
         const int r = 64 * s + ln;
@@ -306,7 +310,7 @@ __device__ __forceinline__ void lu_publish(const double (&acc)[S4][CW], const in
 }
 
 __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Smem &sm, const LuSrc &src, const bool FUSED) {
-    const int t = threadIdx.x;
+    const int t = lvg_tid();
     for (int i = t; i < N; i += BT) {
         sm.perm[i] = i;
         sm.pos[i] = i;

@@ -47,16 +47,18 @@ def test_wave_level_counts(nlev):
     _run("ph2o45_1024", nlev, 8, "", 1, thin=nlev > 52)
 
 
-# the overlap scheme (OH hyperfine pairs, 4-D table, single lines) on the wave kernel: every lane
-# runs the single / near / far paths with clamped indices (lvg_wave.hip); each NM class up to 40
-# is checked against the oracle (OH-HF level counts are even; at 48 levels the line terms no longer
-# fit the wave kernel's LDS and the block kernel takes the solve)
-WAVE_OV_N = [12, 22, 32, 40]                        # NM = 16, 24, 32, 40
+# the overlap scheme (OH hyperfine pairs, 4-D table, single lines) across the NM classes 16-48,
+# each case asserting the kernel that solves it against the oracle: up to 40 levels the wave
+# kernel (every lane runs the single / near / far paths with clamped indices, lvg_wave.hip); at
+# 48 levels the overlap line terms no longer fit the wave kernel's LDS (2 x lines > WYCAP, the
+# host plan lvg_wave_plan rejects it) and the block kernel takes the solve, its 512-thread
+# instantiation since 8 layers leave CUs to spare (lvg_last_kernel_kind 2)
+WAVE_OV_N = [(12, 1), (22, 1), (32, 1), (40, 1), (48, 2)]   # NM = 16, 24, 32, 40, 48
 
 
-@pytest.mark.parametrize("nlev", WAVE_OV_N)
-def test_wave_overlap_level_counts(nlev):
-    _run("oh24_overlap_2048", nlev, 8, "", 1)
+@pytest.mark.parametrize("nlev,kind", WAVE_OV_N)
+def test_wave_overlap_level_counts(nlev, kind):
+    _run("oh24_overlap_2048", nlev, 8, "", kind)
 
 
 @pytest.mark.parametrize("nlev", BLOCK_N)
