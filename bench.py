@@ -299,10 +299,7 @@ def launch_ranks(args, argv) -> int:
         deadline = time.monotonic() + args.launch_timeout
         while live:
             time.sleep(0.2)
-            if time.monotonic() > deadline:
-                print(f"bench.py: ranks still running after {args.launch_timeout:.0f} s; killed", file=sys.stderr)
-                kill_all()
-                return 124
+            # poll first: ranks that finished just before the deadline are not killed
             for p in list(live):
                 c = p.poll()
                 if c is None:
@@ -312,6 +309,10 @@ def launch_ranks(args, argv) -> int:
                     rc = c
                     kill_all()          # a rank failed: the others would wait at a barrier
                     live = []
+            if live and time.monotonic() > deadline:
+                print(f"bench.py: ranks still running after {args.launch_timeout:.0f} s; killed", file=sys.stderr)
+                kill_all()
+                return 124
         return rc if rc >= 0 else 128 - rc
     finally:
         for sig, h in old.items():
@@ -394,6 +395,8 @@ def run_rank(args) -> int:
 
     if stub:
         solver = StubSolver(N)
+        if args.stub_hang > 0:
+            time.sleep(args.stub_hang)          # launcher test: a rank that does not finish
     else:
         from radiative_transfer_amd.native import LvgSolver
         solver = LvgSolver(prob, device=dev.index)
@@ -596,6 +599,7 @@ def main(argv=None):
     ap.add_argument("--no-host-entry", action="store_true")
     ap.add_argument("--no-provenance", action="store_true")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)   # launcher test, CPU only
+    ap.add_argument("--stub-hang", type=float, default=0.0, help=argparse.SUPPRESS)   # stub rank sleeps this long
     args = ap.parse_args(argv)
     if args.weak and args.strong:
         ap.error("--weak and --strong exclude each other")

@@ -522,6 +522,11 @@ int validate(lvg_handle *h, const lvg_problem *p) {
             if (t->nb_d != o[0]->nb_d || t->nb_dx != o[0]->nb_dx || t->nb_gr != o[0]->nb_gr || t->nb_g != o[0]->nb_g ||
                 t->nb_d < 2 || t->nb_dx < 2 || t->nb_gr < 2 || t->nb_g < 2)
                 return fail(h, LVG_E_ARG, "overlap tables must share grids");
+        // the device keeps one copy of the grids (overlap1's) for both tables
+        auto same = [](const double *x, const double *y, int n) { return memcmp(x, y, sizeof(double) * n) == 0; };
+        if (!same(o[0]->log10_delta, o[1]->log10_delta, o[0]->nb_d) || !same(o[0]->dx, o[1]->dx, o[0]->nb_dx) ||
+            !same(o[0]->gratio, o[1]->gratio, o[0]->nb_gr) || !same(o[0]->gamma, o[1]->gamma, o[0]->nb_g))
+            return fail(h, LVG_E_ARG, "overlap tables must share grids");
         if (M.nb_lev % 2) return fail(h, LVG_E_ARG, "line overlap needs an even number of levels (hyperfine doublets)");
     }
     return LVG_OK;

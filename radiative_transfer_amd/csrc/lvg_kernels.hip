@@ -148,6 +148,12 @@ struct Smem {
     Drv    drv;                 // solve_layer's driver state across the LU
 };
 
+// OCC workgroups per CU must fit the CU's LDS (gfx950: 160 KB; the layout above, the L11 of
+// every chunk in particular, is sized for it): a smaller-LDS target fails here instead of
+// silently running fewer workgroups per CU
+constexpr size_t LDS_PER_CU = 160 * 1024;
+static_assert(sizeof(Smem) * OCC <= LDS_PER_CU, "Smem x workgroups per CU exceeds the CU's LDS");
+
 __device__ __forceinline__ double block_max(double v, Smem &sm) {
     const int t = lvg_tid(), w = t >> 6;
     v = wave_max(v);

@@ -325,6 +325,9 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
         const int nw = min(CW, N - c0);
         TSTAMP(tp0);
         // ---- a consistent snapshot of the tile -> physical row map: kp chunks are final
+        //      (seqlock reader: an even sequence word read before and after the perm reads
+        //      means no publish overlapped them, given the writer's in-order LDS stores, see
+        //      the writer below)
         int prow[S4], kp;
         for (;;) {
             const int s1 = lu_ld(sm.seq);
@@ -432,6 +435,12 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
         lu_panel(acc, prow, c0, nb, SLO, N, b, part, lp, rb, sm);
         TACC(PH_PANEL, tp1);
         TSTAMP(tw0);
+        // Seqlock writer. The odd marker must be visible before any perm / pos write of
+        // lu_publish, which are plain LDS stores: a release fence orders earlier accesses
+        // before LATER ATOMIC stores only, so this order rests on the hardware: a wave's LDS
+        // instructions execute in issue order on gfx9 (the fence keeps the compiler from
+        // moving the stores above the marker). If perm / pos ever move out of LDS (global
+        // memory is not in order), write them with relaxed workgroup-scope atomic stores.
         if (l == 0) __hip_atomic_store(&sm.seq, 2 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         lu_publish(acc, prow, j, nb, SLO, A, N, b, part, lp, rb, sm);

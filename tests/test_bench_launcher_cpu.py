@@ -100,9 +100,9 @@ def test_world_size_mismatch_is_an_error():
 
 
 def test_launcher_deadline_kills_ranks():
-    """A rank that never finishes (here: the deadline is shorter than the ranks' start-up)
-    does not hang the launcher: it kills its ranks and exits 124 (ADVICE r3)."""
+    """A rank that never finishes (the stub ranks sleep 120 s, far past the 3 s deadline)
+    does not hang the launcher: it kills its ranks and exits 124 (ADVICE r3, r4)."""
     rc, lines, err = _run("--gpus", "2", "--stub", "--steps", "1", "--workload", "ph2o45_1024", "--layers", "4",
-                          "--no-cpu", "--launch-timeout", "0.5")
+                          "--no-cpu", "--launch-timeout", "3", "--stub-hang", "120", timeout=100)
     assert rc == 124 and not lines
     assert "killed" in err

@@ -21,7 +21,7 @@ import numpy as np
 import pytest
 
 from radiative_transfer_amd import abi, synth
-from radiative_transfer_amd.native import LvgSolver
+from radiative_transfer_amd.native import LvgError, LvgSolver
 from oracle import oracle
 from parity_helpers import assert_same, overlap_dx
 
@@ -158,6 +158,42 @@ def test_overlap_dx_regions():
     s = LvgSolver(P)
     _cmp(s, P, sub, abi.default_opts(**o))
     s.close()
+
+
+def _swap_grid_entries(P, field, i):
+    """Entries i and i+1 of one overlap grid swapped, identically in both tables (the
+    device keeps one copy of the grids): a non-monotone grid."""
+    for t in (P.overlap1, P.overlap2):
+        g = np.array(getattr(t, field), dtype=np.float64, copy=True)
+        g[i], g[i + 1] = g[i + 1], g[i]
+        setattr(t, field, g)
+
+
+@pytest.mark.parametrize("field", ["gamma", "gratio"])
+def test_overlap_nonmonotone_grid(field):
+    """the wave kernel's grid-interval hints fall back to plain bisection when its
+    LDS grid copies are not non-decreasing (lvg_wave.hip, the per-block check). A gamma or
+    gamma-ratio grid with two entries swapped takes that branch; the result is still the
+    oracle's locate_index on the same grid, bit for bit."""
+    P, L, o = synth.make_problem("oh24_overlap_2048", nb_lay=24)
+    g = getattr(P.overlap1, field)
+    _swap_grid_entries(P, field, len(g) // 2)
+    assert (np.diff(getattr(P.overlap1, field)) < 0).any()
+    s = LvgSolver(P)
+    _cmp(s, P, L, abi.default_opts(**o))
+    assert s.last_kernel_kind() == 1
+    s.close()
+
+
+def test_overlap_tables_must_share_grid_values():
+    """The device keeps overlap1's grids for both tables, so lvg_create rejects a second
+    table whose grids differ in value (not only in size)."""
+    P, L, o = synth.make_problem("oh24_overlap_2048", nb_lay=2)
+    g = np.array(P.overlap2.gamma, dtype=np.float64, copy=True)
+    g[-1] *= 1.5
+    P.overlap2.gamma = g
+    with pytest.raises(LvgError, match="share grids"):
+        LvgSolver(P)
 
 
 @pytest.mark.parametrize("name", ["ph2o45_1024", "ch3oha256_4096"])
