@@ -497,6 +497,24 @@ struct Slot {
     double *K, *A, *prev, *res, *opt, *y, *given, *df;
 };
 
+// A value every lane holds alike, read back from LDS: as a scalar (v_readfirstlane), so that
+// the compiler keeps it in SGPRs and branches on it stay uniform (an LDS load is a VGPR, which
+// the compiler must treat as divergent).
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ double uni(double v) {
+    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                            __builtin_amdgcn_readfirstlane(__double2loint(v)));
+}
+__device__ __forceinline__ Ctl uni(const Ctl &c) {
+    Ctl u;
+    u.acceleration = uni(c.acceleration); u.accel_start = uni(c.accel_start); u.accel_period = uni(c.accel_period);
+    u.nb_prev = uni(c.nb_prev); u.max_iter = uni(c.max_iter); u.iter_nb = uni(c.iter_nb);
+    u.nb_after_accel = uni(c.nb_after_accel);
+    u.best_eq = uni(c.best_eq); u.eq_error = uni(c.eq_error); u.pop_error = uni(c.pop_error); u.rel_error = uni(c.rel_error);
+    u.hp = uni(c.hp); u.np = uni(c.np); u.hr = uni(c.hr); u.nr = uni(c.nr);
+    return u;
+}
+
 __device__ __forceinline__ double *ring(double *base, int head, int i, int N) {
     return base + (int64_t)((head + i) & (NHIST - 1)) * N;
 }

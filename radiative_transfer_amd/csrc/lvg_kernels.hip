@@ -1017,14 +1017,8 @@ __device__ __forceinline__ bool solve_layer(const LvgDevProblem &P, const LvgLau
             if (Bdg) { src.BK = Kl; src.BE = P.einst; src.BD = Bdg; }
         }
         for (int i = t; i < N; i += BT) sm.bvec[i] = (i == 0) ? 1. : 0.;
-        if (t == 0) { sm.drv.C = C; sm.drv.boundary = boundary; sm.drv.iters = iters; sm.drv.retry = retry; }
         __syncthreads();
         const double eq = block_lu_solve(S.A, N, sm.bvec, sm, src, !boundary);
-        __asm__ volatile("" ::: "memory");       // reload the driver state (no register copy across the LU)
-        C = sm.drv.C;
-        boundary = sm.drv.boundary;
-        iters = sm.drv.iters;
-        retry = sm.drv.retry;
         if (boundary) {
             TACC(PH_BOUNDARY, tb0);
             for (int i = t; i < N; i += BT) { sm.pold[i] = sm.blog[i]; S.given[i] = sm.blog[i]; }
@@ -1092,7 +1086,7 @@ __global__ void __launch_bounds__(BT, OCC) solve_kernel(const LvgDevProblem *__r
                 sm.pidx = q;
             }
             __syncthreads();
-            const int item = sm.layer, q = sm.pidx;
+            const int item = uni(sm.layer), q = uni(sm.pidx);
             __syncthreads();
             if (q >= nq) break;
             // warm chain: layers in order, each from its predecessor if that converged
@@ -1114,7 +1108,7 @@ __global__ void __launch_bounds__(BT, OCC) solve_kernel(const LvgDevProblem *__r
             sm.pidx = q;
         }
         __syncthreads();
-        const int l = sm.layer, q = sm.pidx;
+        const int l = uni(sm.layer), q = uni(sm.pidx);
         __syncthreads();
         if (q >= nq) break;
         if (!Lc.chain_off) {
@@ -1178,7 +1172,7 @@ __global__ void __launch_bounds__(BT, OCC) lum_kernel(const LvgDevProblem *__res
     for (;;) {
         if (t == 0) sm.layer = atomicAdd(Lc.counter, 1);
         __syncthreads();
-        const int l = sm.layer;
+        const int l = uni(sm.layer);
         __syncthreads();
         if (l >= nl) break;
         layer_setup(P, Lc, l, sm);

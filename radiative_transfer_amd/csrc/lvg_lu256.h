@@ -225,12 +225,12 @@ __device__ __forceinline__ void lu_apply(double (&acc)[S4][CW], const int (&prow
     TSTAMP(tg0);
     // rows taking the update: below the chunk's pivots (logical position >= kk + nb)
     bool take[S4];
-    unsigned loff[S4];                            // 32-bit offsets of the L rows from A
+    const double *lsrc[S4];
 #pragma unroll
     for (int s = 0; s < S4; s++) {
         const int r = 64 * s + l;
         take[s] = s >= s_up && r < N && (earlier ? r : sm.pos[prow[s]]) >= kk + nb;
-        loff[s] = (unsigned)((take[s] ? prow[s] : 0) * N + kk);
+        lsrc[s] = A + (int64_t)(take[s] ? prow[s] : 0) * N + kk;
     }
     constexpr int MG = 4;                         // columns of L per load group
 #pragma unroll
@@ -241,7 +241,7 @@ __device__ __forceinline__ void lu_apply(double (&acc)[S4][CW], const int (&prow
             for (int s = 0; s < S4; s++) {
                 if (s >= s_up) {
                     if ((N & 1) == 0) {
-                        const double2 *p2 = reinterpret_cast<const double2 *>(A + loff[s] + g);
+                        const double2 *p2 = reinterpret_cast<const double2 *>(lsrc[s] + g);
 #pragma unroll
                         for (int h = 0; h < MG / 2; h++) {
                             const double2 v = take[s] ? p2[h] : make_double2(0., 0.);
@@ -249,7 +249,7 @@ __device__ __forceinline__ void lu_apply(double (&acc)[S4][CW], const int (&prow
                         }
                     } else {
 #pragma unroll
-                        for (int h = 0; h < MG; h++) a[s][h] = take[s] ? A[loff[s] + g + h] : 0.;
+                        for (int h = 0; h < MG; h++) a[s][h] = take[s] ? lsrc[s][g + h] : 0.;
                     }
                 }
             }
@@ -257,19 +257,15 @@ __device__ __forceinline__ void lu_apply(double (&acc)[S4][CW], const int (&prow
             for (int mm = 0; mm < MG; mm++) {
                 const int m = g + mm;
                 if (m < nb) {
-                    // U row m in two halves of 8 (16 registers live instead of 32)
+                    double u[CW];
+                    const double2 *up = reinterpret_cast<const double2 *>(&Ub[m][0]);
 #pragma unroll
-                    for (int hh = 0; hh < CW; hh += CW / 2) {
-                        double u[CW / 2];
-                        const double2 *up = reinterpret_cast<const double2 *>(&Ub[m][hh]);
+                    for (int j = 0; j < CW / 2; j++) { const double2 v = up[j]; u[2 * j] = v.x; u[2 * j + 1] = v.y; }
 #pragma unroll
-                        for (int j = 0; j < CW / 4; j++) { const double2 v = up[j]; u[2 * j] = v.x; u[2 * j + 1] = v.y; }
+                    for (int s = 0; s < S4; s++) {
+                        if (s >= s_up) {
 #pragma unroll
-                        for (int s = 0; s < S4; s++) {
-                            if (s >= s_up) {
-#pragma unroll
-                                for (int c = 0; c < CW / 2; c++) acc[s][hh + c] = fma(-a[s][mm], u[c], acc[s][hh + c]);
-                            }
+                            for (int c = 0; c < CW; c++) acc[s][c] = fma(-a[s][mm], u[c], acc[s][c]);
                         }
                     }
                 }
