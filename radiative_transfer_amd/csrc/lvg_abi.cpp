@@ -549,6 +549,13 @@ int build(lvg_handle *h, const lvg_problem *p) {
     if ((rc = upload(h, M.energy, N, &D.energy))) return rc;
     if ((rc = upload(h, g.data(), N, &D.g))) return rc;
     if ((rc = upload(h, M.einst, (size_t)N * N, &D.einst))) return rc;
+    {
+        // transposed copy: the block kernels' boundary-matrix diagonal reads it by columns (coalesced)
+        std::vector<double> et((size_t)N * N);
+        for (int i = 0; i < N; i++)
+            for (int j = 0; j < N; j++) et[(size_t)j * N + i] = M.einst[(size_t)i * N + j];
+        if ((rc = upload(h, et.data(), (size_t)N * N, &D.einst_t))) return rc;
+    }
     // collision tables, T-major, restricted to the levels the molecule uses
     std::vector<int> jmax, nbl;
     std::vector<int64_t> tgo, co;

@@ -61,6 +61,7 @@ struct LvgDevProblem {
     const double *energy;      // [N]
     const double *g;           // [N]
     const double *einst;       // [N*N]
+    const double *einst_t;     // [N*N] transposed: einst_t[r*N + d] = einst[d*N + r]
     // collision tables
     const int     *tab_jmax, *tab_nb_lev;
     const int64_t *tab_tg_off, *tab_c_off;

@@ -180,6 +180,36 @@ __device__ __forceinline__ void layer_collisions(const LvgDevProblem &P, Smem &s
     build_collision_operators<BT, COLL_PU>(P, sm, K, B, cls, electrons);
 }
 
+// Diagonal of the boundary-layer matrix B formed from K (no electron tables: B = K + A/2 above
+// the diagonal, K below it; iteration_control.cpp:69-85): minus the column sum of B for r
+// ascending, the operations build_collision_operators applies to B itself (and coll_kernel to
+// form B_all's diagonal), into dg[N]
+__device__ __forceinline__ void boundary_diagonal(const LvgDevProblem &P, const double *K, double *dg) {
+    const int N = P.N;
+    for (int d = lvg_tid(); d < N; d += BT) {
+        double a = 0.;
+        for (int r0 = 0; r0 < N; r0 += 16) {
+            double kv[16], ev[16];
+#pragma unroll
+            for (int u = 0; u < 16; u++) {
+                const int r = r0 + u < N ? r0 + u : 0;
+                kv[u] = K[(int64_t)r * N + d];
+                ev[u] = P.einst_t[(int64_t)r * N + d];     // einst[d][r], coalesced over d
+            }
+#pragma unroll
+            for (int u = 0; u < 16; u++) {
+                const int r = r0 + u;
+                if (r < N && r != d) {
+                    const double bb = (r < d) ? 0.5 * ev[u] + kv[u] : kv[u];
+                    a = a - bb;
+                }
+            }
+        }
+        dg[d] = a;
+    }
+    __syncthreads();
+}
+
 // y[2n] = A_ul(1+I), y[2n+1] = A_lu*I for every line of the scheme
 __device__ __forceinline__ void compute_line_terms(const LvgDevProblem &P, const LvgModeLines &M, const Smem &sm,
                                                    const double *pop, double *y) {
@@ -975,6 +1005,12 @@ __device__ __forceinline__ bool solve_layer(const LvgDevProblem &P, const LvgLau
             if (Lc.ball) Bsrc = Lc.ball + (int64_t)l * N * N;   // the boundary LU loads B from here
             else Bdg = Lc.bdiag + (int64_t)l * N;               // ... or forms it from K
         }
+    } else if (need_boundary && !from_prev && P.nb_tables == P.nb_neutral) {
+        // no electron tables: the boundary LU forms B from K in its chunk load (as from coll_kernel's
+        // K), so B is never written to the slot and read back; only its diagonal is kept, in LDS
+        layer_collisions(P, sm, S.K, nullptr);
+        boundary_diagonal(P, S.K, sm.diag);
+        Bdg = sm.diag;
     } else {
         layer_collisions(P, sm, S.K, (need_boundary && !from_prev) ? S.A : nullptr);
     }

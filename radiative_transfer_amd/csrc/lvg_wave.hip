@@ -83,9 +83,9 @@ __device__ __forceinline__ void wave_sync_global() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// through the opaque thread index (lvg_common.h): lane-derived addresses and masks are not
-// hoisted out of the layer loop, which had solve_wave_kernel<48> spilling 55 VGPRs (200 B/lane)
-__device__ __forceinline__ int lane_id() { return lvg_tid() & 63; }
+// the plain thread index: through the opaque one (lvg_tid) solve_wave_kernel<48> spills no VGPRs
+// (55 otherwise, 200 B/lane) but runs 1-2% slower (profiles/r5/variants.txt item 9)
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 // Collision operator of the layer (build_collision_operators, one pair per lane):
 // K[s][f] = down + electrons, K[f][s] = up + electrons (LDS, stride ldk = NM | 1); the
