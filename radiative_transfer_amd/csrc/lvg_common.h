@@ -54,6 +54,18 @@ __device__ __forceinline__ int lvg_tid() {
     return v;
 }
 
+// Global-memory pointers (address space 1). The slot, table and layer pointers reach the kernels
+// through structs in device memory, so the compiler cannot infer their address space and emits
+// FLAT accesses: those complete out of order with LDS operations, so every use of a loaded value
+// waits for ALL of the wave's outstanding memory and LDS operations (s_waitcnt vmcnt(0)
+// lgkmcnt(0)). Through a gp<T> pointer it emits global loads with counted vmcnt waits.
+template <class T> using gp = __attribute__((address_space(1))) T *;
+template <class T> __device__ __forceinline__ gp<T> glb(T *p) { return (gp<T>)p; }
+// 16-byte vectors for loads and stores through gp pointers (builtin vector types: HIP's double2 /
+// int4 classes cannot be copied from an address-space-qualified object)
+typedef double vd2 __attribute__((ext_vector_type(2)));
+typedef int vi4 __attribute__((ext_vector_type(4)));
+
 constexpr double BOLTZMANN_CONSTANT    = 1.380649e-16;
 constexpr double CM_INVERSE_TO_KELVINS = 1.438776877;
 constexpr double EIGHT_PI              = 25.132741228718345;

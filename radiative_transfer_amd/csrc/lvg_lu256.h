@@ -215,7 +215,7 @@ __device__ __forceinline__ void lu_apply(double (&acc)[S4][CW], const int (&prow
         if (r < nb) {
 #pragma unroll
             for (int i = 0; i < CL; i++) Ub[r][CL * q4 + i] = x[i];
-            double *urow = A + (int64_t)sm.perm[kk + r] * N + cw0 + CL * q4;
+            gp<double> urow = glb(A) + (int64_t)sm.perm[kk + r] * N + cw0 + CL * q4;
 #pragma unroll
             for (int i = 0; i < CL; i++) if (CL * q4 + i < nw) urow[i] = x[i];
         }
@@ -225,12 +225,12 @@ __device__ __forceinline__ void lu_apply(double (&acc)[S4][CW], const int (&prow
     TSTAMP(tg0);
     // rows taking the update: below the chunk's pivots (logical position >= kk + nb)
     bool take[S4];
-    const double *lsrc[S4];
+    gp<const double> lsrc[S4];
 #pragma unroll
     for (int s = 0; s < S4; s++) {
         const int r = 64 * s + l;
         take[s] = s >= s_up && r < N && (earlier ? r : sm.pos[prow[s]]) >= kk + nb;
-        lsrc[s] = A + (int64_t)(take[s] ? prow[s] : 0) * N + kk;
+        lsrc[s] = glb((const double *)A) + (int64_t)(take[s] ? prow[s] : 0) * N + kk;
     }
     constexpr int MG = 4;                         // columns of L per load group
 #pragma unroll
@@ -241,15 +241,19 @@ __device__ __forceinline__ void lu_apply(double (&acc)[S4][CW], const int (&prow
             for (int s = 0; s < S4; s++) {
                 if (s >= s_up) {
                     if ((N & 1) == 0) {
-                        const double2 *p2 = reinterpret_cast<const double2 *>(lsrc[s] + g);
+                        // global (not flat) loads, exec-masked to the rows taking the update: a flat
+                        // load would also wait for the LDS queue (profiles/r5/variants.txt item 13)
+                        gp<const vd2> p2 = reinterpret_cast<gp<const vd2>>(lsrc[s] + g);
 #pragma unroll
                         for (int h = 0; h < MG / 2; h++) {
-                            const double2 v = take[s] ? p2[h] : make_double2(0., 0.);
-                            a[s][2 * h] = v.x; a[s][2 * h + 1] = v.y;
+                            const vd2 z = {0., 0.};
+                            const vd2 v = take[s] ? p2[h] : z;
+                            a[s][2 * h] = v.x;
+                            a[s][2 * h + 1] = v.y;
                         }
                     } else {
 #pragma unroll
-                        for (int h = 0; h < MG; h++) a[s][h] = take[s] ? lsrc[s][g + h] : 0.;
+                        for (int h = 0; h < MG; h++) { const double v = lsrc[s][g + h]; a[s][h] = take[s] ? v : 0.; }
                     }
                 }
             }
@@ -287,13 +291,14 @@ __device__ __forceinline__ void lu_publish(const double (&acc)[S4][CW], const in
         if (s < s_lo || r >= N || !part[s]) continue;
         const int p = prow[s], q = lp[s];
         const double (&v)[CW] = acc[s];
+        gp<double> Ap = glb(A) + (int64_t)p * N + kk;
         if ((N & 1) == 0 && nb == CW) {
-            double2 *d2 = reinterpret_cast<double2 *>(A + (int64_t)p * N + kk);
+            gp<vd2> d2 = reinterpret_cast<gp<vd2>>(Ap);
 #pragma unroll
-            for (int j = 0; j < CW / 2; j++) d2[j] = make_double2(v[2 * j], v[2 * j + 1]);
+            for (int j = 0; j < CW / 2; j++) { const vd2 x = {v[2 * j], v[2 * j + 1]}; d2[j] = x; }
         } else {
 #pragma unroll
-            for (int j = 0; j < CW; j++) if (j < nb) A[(int64_t)p * N + kk + j] = v[j];
+            for (int j = 0; j < CW; j++) if (j < nb) Ap[j] = v[j];
         }
         sm.perm[kk + q] = p;
         sm.pos[p] = kk + q;
