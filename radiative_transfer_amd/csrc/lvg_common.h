@@ -64,6 +64,7 @@ template <class T> __device__ __forceinline__ gp<T> glb(T *p) { return (gp<T>)p;
 // 16-byte vectors for loads and stores through gp pointers (builtin vector types: HIP's double2 /
 // int4 classes cannot be copied from an address-space-qualified object)
 typedef double vd2 __attribute__((ext_vector_type(2)));
+typedef double vd2u __attribute__((ext_vector_type(2), aligned(8)));
 typedef int vi4 __attribute__((ext_vector_type(4)));
 
 constexpr double BOLTZMANN_CONSTANT    = 1.380649e-16;

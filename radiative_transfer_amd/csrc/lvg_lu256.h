@@ -167,6 +167,13 @@ __device__ __forceinline__ void lu_wait(const int &x, int v) {
     while (lu_ld(x) < v) __builtin_amdgcn_s_sleep(1);
 }
 
+// L source of the rows that take no update in lu_apply (and of the slots below s_up): every
+// lane of every slot loads, from its row or from these zeros. Exec-masked loads behind
+// s_cbranch_execz left the number of loads in flight path-dependent, so the waitcnt pass
+// drained the queue (vmcnt(0)) at every slot block of the FMA stream; unconditional loads
+// through global (not flat) pointers measured +6% (profiles/r5/variants.txt item 14).
+__device__ __attribute__((aligned(16))) double lu_zero_row[CW] = {0.};
+
 // Chunk ci (columns kk.., nb of them, published) applied to this wave's columns cw0.. (nw).
 // earlier: ci was published before this chunk's load, so its pivot rows sit at tile rows
 // kk..kk+15 and the rows taking its update at tile rows >= kk + 16. s_up: first row slot
@@ -230,50 +237,43 @@ __device__ __forceinline__ void lu_apply(double (&acc)[S4][CW], const int (&prow
     for (int s = 0; s < S4; s++) {
         const int r = 64 * s + l;
         take[s] = s >= s_up && r < N && (earlier ? r : sm.pos[prow[s]]) >= kk + nb;
-        lsrc[s] = glb((const double *)A) + (int64_t)(take[s] ? prow[s] : 0) * N + kk;
+        lsrc[s] = take[s] ? glb((const double *)A) + (int64_t)prow[s] * N + kk : glb((const double *)lu_zero_row);
     }
     constexpr int MG = 4;                         // columns of L per load group
+    auto load = [&](double (&a)[S4][MG], int g) __attribute__((always_inline)) {
+#pragma unroll
+        for (int s = 0; s < S4; s++) {
+            // 16-byte loads at 8-byte alignment (odd N): global memory takes them unaligned
+            gp<const vd2u> p2 = reinterpret_cast<gp<const vd2u>>(lsrc[s] + g);
+#pragma unroll
+            for (int h = 0; h < MG / 2; h++) { const vd2u v = p2[h]; a[s][2 * h] = v.x; a[s][2 * h + 1] = v.y; }
+        }
+    };
+    auto update = [&](const double (&a)[S4][MG], int g) __attribute__((always_inline)) {
+#pragma unroll
+        for (int mm = 0; mm < MG; mm++) {
+            const int m = g + mm;
+            if (m < nb) {
+                double u[CW];
+                const double2 *up = reinterpret_cast<const double2 *>(&Ub[m][0]);
+#pragma unroll
+                for (int j = 0; j < CW / 2; j++) { const double2 v = up[j]; u[2 * j] = v.x; u[2 * j + 1] = v.y; }
+#pragma unroll
+                for (int s = 0; s < S4; s++) {
+                    if (s >= s_up) {
+#pragma unroll
+                        for (int c = 0; c < CW; c++) acc[s][c] = fma(-a[s][mm], u[c], acc[s][c]);
+                    }
+                }
+            }
+        }
+    };
+    double a[S4][MG];
 #pragma unroll
     for (int g = 0; g < CW; g += MG) {
         if (g < nb) {
-            double a[S4][MG];
-#pragma unroll
-            for (int s = 0; s < S4; s++) {
-                if (s >= s_up) {
-                    if ((N & 1) == 0) {
-                        // global (not flat) loads, exec-masked to the rows taking the update: a flat
-                        // load would also wait for the LDS queue (profiles/r5/variants.txt item 13)
-                        gp<const vd2> p2 = reinterpret_cast<gp<const vd2>>(lsrc[s] + g);
-#pragma unroll
-                        for (int h = 0; h < MG / 2; h++) {
-                            const vd2 z = {0., 0.};
-                            const vd2 v = take[s] ? p2[h] : z;
-                            a[s][2 * h] = v.x;
-                            a[s][2 * h + 1] = v.y;
-                        }
-                    } else {
-#pragma unroll
-                        for (int h = 0; h < MG; h++) { const double v = lsrc[s][g + h]; a[s][h] = take[s] ? v : 0.; }
-                    }
-                }
-            }
-#pragma unroll
-            for (int mm = 0; mm < MG; mm++) {
-                const int m = g + mm;
-                if (m < nb) {
-                    double u[CW];
-                    const double2 *up = reinterpret_cast<const double2 *>(&Ub[m][0]);
-#pragma unroll
-                    for (int j = 0; j < CW / 2; j++) { const double2 v = up[j]; u[2 * j] = v.x; u[2 * j + 1] = v.y; }
-#pragma unroll
-                    for (int s = 0; s < S4; s++) {
-                        if (s >= s_up) {
-#pragma unroll
-                            for (int c = 0; c < CW; c++) acc[s][c] = fma(-a[s][mm], u[c], acc[s][c]);
-                        }
-                    }
-                }
-            }
+            load(a, g);
+            update(a, g);
         }
     }
     TACC(PH_GEMM, tg0);

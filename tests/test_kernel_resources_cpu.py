@@ -6,7 +6,8 @@ VERDICT r4 item 1 asked for lvg::solve_kernel without scratch. Round 5 built tha
 in halves: 1 VGPR spilled, 8 B/lane) and measured it 1.8% SLOWER than the round-4 kernel; the
 product keeps the two changes that made it faster (opaque thread index, one call site: 128 -> 56
 VGPRs spilled, 280 -> 100 B/lane, +3.4%) and drops the two that only removed spills
-(profiles/r5/variants.txt items 1-2). These tests pin that budget so that a change which pushes
+(profiles/r5/variants.txt items 1-2). The later rank-16 rework (unconditional global L loads, item 14) runs
++6% faster at 83 VGPRs spilled (156 B/lane). These tests pin that budget so that a change which pushes
 the LU back into heavy scratch use (round 4: 128 VGPRs, 564 SGPRs, 280 B/lane) fails here, on
 the CPU, before any GPU run; and they pin the LDS layout to two workgroups per CU.
 """
@@ -38,8 +39,8 @@ def notes():
 def test_block_solve_kernel_scratch_budget(notes, name):
     k = notes[name]
     assert k["vgpr"] <= 256 and k["agpr"] == 0
-    assert k["vgpr_spill"] <= 64, k
-    assert k["scratch"] <= 128, k
+    assert k["vgpr_spill"] <= 96, k
+    assert k["scratch"] <= 192, k
     assert k["sgpr_spill"] <= 256, k
 
 
