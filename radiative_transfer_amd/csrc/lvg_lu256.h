@@ -347,23 +347,33 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
             const int r = 64 * s + l, pr = prow[s];
             const bool okr = r < N;
             if (!FUSED) {
+                // every load unconditional (rows past N read row 0 or the zero row, columns past N
+                // column N - 1), the values selected after: no exec-masked loads (lu_zero_row)
+                double kv[CW];
+                gp<const double> rsrc = glb(src.BK ? src.BK : (src.B ? src.B : A));
+                if (nw == CW) {
+                    gp<const vd2u> k2 = reinterpret_cast<gp<const vd2u>>(
+                        okr ? rsrc + (int64_t)pr * N + c0 : glb((const double *)lu_zero_row));
 #pragma unroll
-                for (int jj = 0; jj < CW; jj++) {
-                    const int d = c0 + jj;
-                    const bool ok = okr && jj < nw;
-                    double v;
-                    if (src.BK) {
-                        const double k = ok ? src.BK[(int64_t)pr * N + d] : 0.;
-                        const double e = (ok && pr < d) ? src.BE[(int64_t)d * N + pr] : 0.;
-                        const double dg = (ok && pr == d) ? src.BD[d] : 0.;
-                        v = (pr < d) ? 0.5 * e + k : k;   // build_collision_operators: 0.5 * af + dn
+                    for (int jj = 0; jj < CW / 2; jj++) { const vd2u x = k2[jj]; kv[2 * jj] = x.x; kv[2 * jj + 1] = x.y; }
+                } else {
+#pragma unroll
+                    for (int jj = 0; jj < CW; jj++) kv[jj] = rsrc[(int64_t)pr * N + min(c0 + jj, N - 1)];
+                }
+                if (src.BK) {
+#pragma unroll
+                    for (int jj = 0; jj < CW; jj++) {
+                        const int d = c0 + jj, dc = min(d, N - 1);
+                        const double e = glb(src.BE)[(int64_t)dc * N + pr];
+                        const double dg = src.BD[dc];
+                        double v = (pr < d) ? 0.5 * e + kv[jj] : kv[jj];   // build_collision_operators: 0.5 * af + dn
                         if (pr == d) v = dg;
                         if (pr == 0) v = 1.;
-                    } else {
-                        v = ok ? (src.B ? src.B : A)[(int64_t)pr * N + d] : 0.;
+                        kv[jj] = v;
                     }
-                    acc[s][jj] = ok ? v : 0.;
                 }
+#pragma unroll
+                for (int jj = 0; jj < CW; jj++) acc[s][jj] = (okr && jj < nw) ? kv[jj] : 0.;
             } else {
                 int li[CW];
                 const int64_t o = (int64_t)(okr ? pr : 0) * N + c0;
