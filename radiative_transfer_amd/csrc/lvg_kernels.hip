@@ -1009,7 +1009,9 @@ __device__ __forceinline__ bool solve_layer(const LvgDevProblem &P, const LvgLau
         // no electron tables: the boundary LU forms B from K in its chunk load (as from coll_kernel's
         // K), so B is never written to the slot and read back; only its diagonal is kept, in LDS
         layer_collisions(P, sm, S.K, nullptr);
+        TSTAMP(tbd0);
         boundary_diagonal(P, S.K, sm.diag);
+        TACC(PH_BDIAG, tbd0);
         Bdg = sm.diag;
     } else {
         layer_collisions(P, sm, S.K, (need_boundary && !from_prev) ? S.A : nullptr);
