@@ -239,6 +239,10 @@ __device__ __forceinline__ void lu_apply(double (&acc)[S4][CW], const int (&prow
         take[s] = s >= s_up && r < N && (earlier ? r : sm.pos[prow[s]]) >= kk + nb;
         lsrc[s] = take[s] ? glb((const double *)A) + (int64_t)prow[s] * N + kk : glb((const double *)lu_zero_row);
     }
+    // slots with no row taking the update skip their FMAs (uniform: one ballot per slot)
+    bool upd[S4];
+#pragma unroll
+    for (int s = 0; s < S4; s++) upd[s] = s >= s_up && __ballot(take[s]) != 0;
     constexpr int MG = 4;                         // columns of L per load group
     auto load = [&](double (&a)[S4][MG], int g) __attribute__((always_inline)) {
 #pragma unroll
@@ -260,7 +264,7 @@ __device__ __forceinline__ void lu_apply(double (&acc)[S4][CW], const int (&prow
                 for (int j = 0; j < CW / 2; j++) { const double2 v = up[j]; u[2 * j] = v.x; u[2 * j + 1] = v.y; }
 #pragma unroll
                 for (int s = 0; s < S4; s++) {
-                    if (s >= s_up) {
+                    if (upd[s]) {
 #pragma unroll
                         for (int c = 0; c < CW; c++) acc[s][c] = fma(-a[s][mm], u[c], acc[s][c]);
                     }
