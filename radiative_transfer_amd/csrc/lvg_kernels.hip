@@ -92,6 +92,7 @@ struct Drv {
     int boundary, iters, retry;
 };
 
+constexpr int EGRID_CAP = 256;   // escape grids copied to LDS (esc_nd + esc_ng doubles)
 #if LVG_BIG
 struct Smem {
     double pold[NMAX], bvec[NMAX];
@@ -131,6 +132,11 @@ struct Smem {
         double hist_acc[32];    // accel_step sums (used outside the LU only)
     } pu;
 #endif
+    // the escape-probability grids (esc_delta, esc_gamma) when they fit: the bisections of
+    // every line's escape probability step through LDS instead of L2 (esc_in_lds; +1.2%,
+    // profiles/r5/variants.txt item 25)
+    double egrid[EGRID_CAP];
+    int esc_in_lds;
     // per-layer scalars
     double T, Te, vw, vgrad, nmol, ne;
     double cc[LVG_MAX_COMBOS];
@@ -210,10 +216,19 @@ __device__ __forceinline__ void boundary_diagonal(const LvgDevProblem &P, const 
     __syncthreads();
 }
 
+// the escape grids into LDS once per launch (compute_line_terms reads them from there)
+__device__ __forceinline__ void load_esc_grids(const LvgDevProblem &P, Smem &sm) {
+    const int nd = P.esc_nd, ng = P.esc_ng;
+    const bool fit = nd + ng <= EGRID_CAP;
+    if (fit)
+        for (int e = lvg_tid(); e < nd + ng; e += BT) sm.egrid[e] = e < nd ? P.esc_delta[e] : P.esc_gamma[e - nd];
+    if (lvg_tid() == 0) sm.esc_in_lds = fit;
+    __syncthreads();
+}
+
 // y[2n] = A_ul(1+I), y[2n+1] = A_lu*I for every line of the scheme
-__device__ __forceinline__ void compute_line_terms(const LvgDevProblem &P, const LvgModeLines &M, const Smem &sm,
-                                                   const double *pop, double *y) {
-    const EscGrids G = global_grids(P);
+__device__ __forceinline__ void line_terms_with(const LvgDevProblem &P, const EscGrids &G, const LvgModeLines &M,
+                                                const Smem &sm, const double *pop, double *y) {
     for (int q = lvg_tid(); q < M.nb_units; q += BT) {
         int n1 = M.unit_l0[q], n2 = M.unit_l1[q];
         if (n2 < 0) {
@@ -228,6 +243,17 @@ __device__ __forceinline__ void compute_line_terms(const LvgDevProblem &P, const
             y[2 * n2] = M.line_aul[n2] * (1. + i2);
             y[2 * n2 + 1] = M.line_alu[n2] * i2;
         }
+    }
+}
+__device__ __forceinline__ void compute_line_terms(const LvgDevProblem &P, const LvgModeLines &M, const Smem &sm,
+                                                   const double *pop, double *y) {
+    EscGrids G = global_grids(P);
+    if (sm.esc_in_lds) {
+        G.ed = sm.egrid;
+        G.eg = sm.egrid + P.esc_nd;
+        line_terms_with(P, G, M, sm, pop, y);
+    } else {
+        line_terms_with(P, G, M, sm, pop, y);
     }
 }
 
@@ -1109,6 +1135,7 @@ __global__ void __launch_bounds__(BT, OCC) solve_kernel(const LvgDevProblem *__r
     const LvgLaunch &Lc = *Lp;
     PH_INIT();
     load_rule_table<BT>(P, sm);
+    load_esc_grids(P, sm);
     Slot S = make_slot(P, Lc, blockIdx.x);
     const int nq = Lc.chain_off ? Lc.nb_chain : Lc.nb_lay;
 #if !LVG_BIG
@@ -1169,6 +1196,7 @@ __global__ void __launch_bounds__(BT, OCC) debug_kernel(const LvgDevProblem *__r
     const LvgDevProblem &P = *Pp;
     const LvgLaunch &Lc = *Lp;
     load_rule_table<BT>(P, sm);
+    load_esc_grids(P, sm);
     Slot S = make_slot(P, Lc, 0);
     const int N = P.N, t = lvg_tid();
     const LvgModeLines &M = Lc.line_overlap ? P.overlap : P.plain;
