@@ -361,11 +361,21 @@ def run_rank(args) -> int:
         return 2
     multi = world > 1
     stub = args.stub
-    if multi:
+    # a process group at world size 1 too (--process-group): the step's status all-reduce then
+    # runs through RCCL on device tensors exactly as it does on every rank of an N-GPU run
+    use_pg = multi or args.process_group
+    backend = None
+    if use_pg:
         import torch.distributed as td
         if not stub:
             torch.cuda.set_device(local)
+        if not multi:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         td.init_process_group(backend="gloo" if stub else "nccl")
+        backend = td.get_backend()
     elif not stub:
         torch.cuda.set_device(0)
     dev = torch.device("cpu") if stub else torch.device("cuda", torch.cuda.current_device())
@@ -429,7 +439,7 @@ def run_rank(args) -> int:
     max_layer_its = int(st1["iterations"].max()) if n_mine else 0
 
     prov = Provenance(enabled=(rank == 0 and not stub and not args.no_provenance))
-    if multi:
+    if use_pg:
         td.barrier()
     sync()
     prov.timed_start()
@@ -441,7 +451,7 @@ def run_rank(args) -> int:
         kern_ms.append(ms)
         coll_ms.append(solver.last_coll_time())
     sync()
-    if multi:
+    if use_pg:
         td.barrier()
     elapsed = time.perf_counter() - t0
     prov_rec = prov.timed_end()
@@ -454,7 +464,7 @@ def run_rank(args) -> int:
     mine_rec = [float(lo), float(hi), float(units_local), float(max_layer_its),
                 float(np.mean(kern_ms)) if n_mine else 0.0, 1e3 * elapsed / args.steps, float(kernel_kind)]
     shares = [mine_rec]
-    if multi:
+    if use_pg:
         rec = torch.tensor(mine_rec, dtype=torch.float64, device=dev)
         outs = [torch.zeros_like(rec) for _ in range(world)]
         td.all_gather(outs, rec)
@@ -483,9 +493,9 @@ def run_rank(args) -> int:
     if rank == 0:
         print(json.dumps(report(args, world, N, total, L_cfg, lo, hi, units_total, units_local, nonconv, max_rel,
                                 max_layer_its, elapsed, kern_ms, coll_ms, opts, offs, prov_rec, host_value,
-                                prob, mine, stub, kernel_kind, shares)), flush=True)
+                                prob, mine, stub, kernel_kind, shares, backend)), flush=True)
     solver.close()
-    if multi:
+    if use_pg:
         td.destroy_process_group()
     return 0
 
@@ -496,7 +506,7 @@ KERNELS = {-1: "none (empty launch)", 0: "lvg::solve_kernel", 1: "lvg::solve_wav
 
 def report(args, world, N, total, L_cfg, lo, hi, units_total, units_local, nonconv, max_rel, max_layer_its,
            elapsed, kern_ms, coll_ms, opts, offs, prov_rec, host_value, prob, mine, stub, kernel_kind=0,
-           shares=None):
+           shares=None, backend=None):
     from radiative_transfer_amd import synth
     value = units_total * args.steps / elapsed
     kms = float(np.mean(kern_ms))
@@ -568,6 +578,9 @@ def report(args, world, N, total, L_cfg, lo, hi, units_total, units_local, nonco
                     "ms_per_step": s[5], "kernel": KERNELS[int(s[6])]} for r, s in enumerate(shares or [])],
         "max_share_ms": max((s[4] for s in shares), default=kms) if shares else kms,
         "provenance": prov_rec,
+        # torch.distributed backend of the step's status all-reduce ("nccl" = RCCL over xGMI);
+        # None: no process group (world size 1 without --process-group)
+        "backend": backend,
     }
     if host_value is not None:
         out["host_entry_value"] = host_value["value"]
@@ -598,6 +611,8 @@ def main(argv=None):
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-entry", action="store_true")
     ap.add_argument("--no-provenance", action="store_true")
+    ap.add_argument("--process-group", action="store_true",
+                    help="create the process group (RCCL) at world size 1 too; the status all-reduce goes through it")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)   # launcher test, CPU only
     ap.add_argument("--stub-hang", type=float, default=0.0, help=argparse.SUPPRESS)   # stub rank sleeps this long
     args = ap.parse_args(argv)

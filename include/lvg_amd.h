@@ -213,6 +213,28 @@ void        lvg_solve_opts_default(lvg_solve_opts *opts);
  * collisional_transitions, dust_model, iteration_scheme_lvg(::init_molecule_data). */
 int         lvg_create(const lvg_problem *prob, int device, lvg_handle **out);
 void        lvg_destroy(lvg_handle *h);
+
+/* ---- several GPUs in one process (lvg_create(..., device_mask, ...)) ----------
+ * One handle over the devices of `device_mask` (bit d = HIP ordinal d of this process): the
+ * tables are replicated on every device, and lvg_solve_layers (independent layers),
+ * lvg_solve_chains and lvg_boundary_layer_populations split their batch into contiguous
+ * blocks, layer l on the (l*G/nb_lay)-th device (lvg_shard_range), whole clouds per device for
+ * chains (lvg_chain_shard), one host thread and one stream per device, no exchange between
+ * devices (the layers are independent). This replaces the reference's serial layer loop
+ * (radiative_transfer.cpp:236-256) across GPUs without MPI / RCCL; a caller that runs one
+ * process per GPU uses lvg_create per rank instead. A warm chain over the
+ * whole cloud (lvg_solve_layers with LVG_INIT_WARM_CHAIN) is sequential and runs on the first
+ * device; every other entry point works on the first device. lvg_last_kernel_time reports
+ * the slowest device's kernel time and the launches of all devices. Results are bit-identical
+ * to one device's. lvg_create_devices takes an explicit list (repeats allowed: several blocks
+ * on one GPU, each with its own stream). */
+int         lvg_create_multi(const lvg_problem *prob, unsigned device_mask, lvg_handle **out);
+int         lvg_create_devices(const lvg_problem *prob, int nb_devices, const int *devices, lvg_handle **out);
+int         lvg_nb_devices(const lvg_handle *h);
+/* the partition rules (pure functions, no device): block [lo, hi) of device r of nb_dev over n
+ * layers; the chains [c_lo, c_hi) of device r (chain c = layers [chain_off[c], chain_off[c+1])) */
+int         lvg_shard_range(int n, int nb_dev, int r, int *lo, int *hi);
+int         lvg_chain_shard(int nb_chain, const int *chain_off, int nb_dev, int r, int *c_lo, int *c_hi);
 const char *lvg_last_error(const lvg_handle *h);   /* h may be NULL: last create error */
 int         lvg_nb_lev(const lvg_handle *h);
 

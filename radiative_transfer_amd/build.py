@@ -30,15 +30,16 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile every source to an object in parallel (hipcc per file), then link."""
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, lib: str = LIB, defines=(), obj_sub: str = "obj") -> str:
+    """Compile every source to an object in parallel (hipcc per file), then link.
+    `defines` / `lib` / `obj_sub` build a diagnostic variant of the same sources (build_checked)."""
+    if not force and lib == LIB and not _stale():
         return LIB
     from concurrent.futures import ThreadPoolExecutor
-    obj_dir = os.path.join(LIB_DIR, "obj")
+    obj_dir = os.path.join(LIB_DIR, obj_sub)
     os.makedirs(obj_dir, exist_ok=True)
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall",
-             "-Wno-unused-function"]
+             "-Wno-unused-function"] + ["-D" + d for d in defines]
     objs = [os.path.join(obj_dir, os.path.splitext(f)[0] + ".o") for f in SOURCES]
 
     def compile_one(i):
@@ -49,12 +50,22 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     with ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 1)) as ex:
         list(ex.map(compile_one, range(len(SOURCES))))
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(lib + ".tmp", lib)
+    return lib
+
+
+CHECKED_LIB = os.path.join(LIB_DIR, "liblvg_amd_checked.so")
+
+
+def build_checked(verbose: bool = False) -> str:
+    """The product sources with -DLVG_CHECKED_GLB: every glb() cast traps on an LDS or scratch
+    pointer (lvg_common.h, the HBM-only rule). Run the GPU suite on it with
+    LVG_LIB_PATH=radiative_transfer_amd/_lib/liblvg_amd_checked.so."""
+    return build(force=True, verbose=verbose, lib=CHECKED_LIB, defines=("LVG_CHECKED_GLB",), obj_sub="obj_checked")
 
 
 HOST_SRCS = [os.path.join(PKG, "host", f) for f in ("lvg_host.cpp", "lvg_ingest.cpp")]
@@ -80,5 +91,8 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
 
 
 if __name__ == "__main__":
+    if "--checked" in sys.argv:
+        print(build_checked(verbose=True))
+        sys.exit(0)
     print(build(force="--force" in sys.argv, verbose=True))
     print(build_host(force="--force" in sys.argv, verbose=True))

@@ -18,6 +18,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 #include <cstdlib>
 
@@ -134,6 +135,10 @@ struct lvg_handle {
     int n_launch_slots = 0;
     LvgTuning tune;
     std::string err;
+    // lvg_create_devices / lvg_create_multi: the handles of the further devices (this handle is
+    // the first device); lvg_solve_layers / lvg_solve_chains / lvg_boundary_layer_populations
+    // split their layers over all of them, one host thread and one stream per device
+    std::vector<lvg_handle *> peers;
 };
 
 namespace {
@@ -508,10 +513,13 @@ int validate(lvg_handle *h, const lvg_problem *p) {
     }
     const int nc = p->dust ? p->dust->nb_comp : 0;
     if (nc > LVG_MAX_DUST) return fail(h, LVG_E_UNSUPPORTED, "more than %d dust components", LVG_MAX_DUST);
+    if (nc > 0 && !p->dust->comp) return fail(h, LVG_E_ARG, "dust components missing");
     for (int c = 0; c < nc; c++) {
         const lvg_dust_component &d = p->dust->comp[c];
-        if (d.nb_en < 2 || !ascending(d.energy, d.nb_en, true)) return fail(h, LVG_E_ARG, "dust component %d malformed", c);
+        if (d.nb_en < 2 || !d.energy || !d.abs_coeff || !ascending(d.energy, d.nb_en, true))
+            return fail(h, LVG_E_ARG, "dust component %d malformed", c);
     }
+    if (!p->esc->delta || !p->esc->gamma || !p->esc->p) return fail(h, LVG_E_ARG, "escape table arrays missing");
     if (p->esc->nb_d < 2 || p->esc->nb_g < 2 || !ascending(p->esc->delta, p->esc->nb_d, true) ||
         !ascending(p->esc->gamma, p->esc->nb_g, true))
         return fail(h, LVG_E_ARG, "escape table malformed");
@@ -519,10 +527,15 @@ int validate(lvg_handle *h, const lvg_problem *p) {
     if (p->overlap1) {
         const lvg_overlap_table *o[2] = {p->overlap1, p->overlap2};
         for (auto t : o)
+            if (!t->log10_delta || !t->dx || !t->gratio || !t->gamma || !t->p)
+                return fail(h, LVG_E_ARG, "overlap table arrays missing");
+        for (auto t : o)
             if (t->nb_d != o[0]->nb_d || t->nb_dx != o[0]->nb_dx || t->nb_gr != o[0]->nb_gr || t->nb_g != o[0]->nb_g ||
                 t->nb_d < 2 || t->nb_dx < 2 || t->nb_gr < 2 || t->nb_g < 2)
                 return fail(h, LVG_E_ARG, "overlap tables must share grids");
-        // the device keeps one copy of the grids (overlap1's) for both tables
+        // The device keeps one copy of the grids (overlap1's) for both tables. The reference's two
+        // lvg_line_overlap_data objects (lvg_method_functions.h:55-70) each carry their own grids;
+        // its two files share them, and this build requires that (DESIGN.md §8 restrictions)
         auto same = [](const double *x, const double *y, int n) { return memcmp(x, y, sizeof(double) * n) == 0; };
         if (!same(o[0]->log10_delta, o[1]->log10_delta, o[0]->nb_d) || !same(o[0]->dx, o[1]->dx, o[0]->nb_dx) ||
             !same(o[0]->gratio, o[1]->gratio, o[0]->nb_gr) || !same(o[0]->gamma, o[1]->gamma, o[0]->nb_g))
@@ -737,7 +750,10 @@ int lvg_set_tuning(lvg_handle *h, const char *spec) {
     // merged into the current settings (the environment's included); "" resets them
     LvgTuning t = (spec && *spec) ? h->tune : LvgTuning();
     const int rc = parse_tuning(h, spec, t);
-    if (rc == LVG_OK) h->tune = t;
+    if (rc == LVG_OK) {
+        h->tune = t;
+        for (lvg_handle *q : h->peers) q->tune = t;
+    }
     return rc;
 }
 
@@ -763,6 +779,8 @@ int lvg_layer_soa_rows(const lvg_handle *h) { return h ? 10 + h->nb_comp : 0; }
 
 void lvg_destroy(lvg_handle *h) {
     if (!h) return;
+    for (lvg_handle *q : h->peers) lvg_destroy(q);
+    h->peers.clear();
     (void)hipSetDevice(h->device);
     drain(h);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
@@ -840,6 +858,67 @@ int lvg_create(const lvg_problem *prob, int device, lvg_handle **out) {
     *out = h;
     return LVG_OK;
 }
+
+int lvg_shard_range(int n, int nb_dev, int r, int *lo, int *hi) {
+    if (n < 0 || nb_dev < 1 || r < 0 || r >= nb_dev || !lo || !hi) return LVG_E_ARG;
+    *lo = (int)(((int64_t)n * r) / nb_dev);
+    *hi = (int)(((int64_t)n * (r + 1)) / nb_dev);
+    return LVG_OK;
+}
+
+int lvg_chain_shard(int nb_chain, const int *chain_off, int nb_dev, int r, int *c_lo, int *c_hi) {
+    if (nb_chain < 0 || !chain_off || !c_lo || !c_hi) return LVG_E_ARG;
+    int lo, hi;
+    const int rc = lvg_shard_range(chain_off[nb_chain], nb_dev, r, &lo, &hi);
+    if (rc) return rc;
+    // first chain starting at or after lo / hi (chain starts are non-decreasing)
+    const int *b = chain_off, *e = chain_off + nb_chain;
+    *c_lo = (int)(std::lower_bound(b, e, lo) - b);
+    *c_hi = (r == nb_dev - 1) ? nb_chain : (int)(std::lower_bound(b, e, hi) - b);
+    return LVG_OK;
+}
+
+int lvg_create_devices(const lvg_problem *prob, int nb_devices, const int *devices, lvg_handle **out) {
+    g_create_error.clear();
+    if (!out) return fail(nullptr, LVG_E_ARG, "out is NULL");
+    *out = nullptr;
+    if (nb_devices < 1 || nb_devices > 64 || !devices) return fail(nullptr, LVG_E_ARG, "need 1..64 device ordinals");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+    for (int i = 0; i < nb_devices; i++)
+        if (devices[i] < 0 || devices[i] >= ndev)
+            return fail(nullptr, LVG_E_DEVICE, "device %d not present (%d visible)", devices[i], ndev);
+    lvg_handle *h = nullptr;
+    int rc = lvg_create(prob, devices[0], &h);
+    if (rc) return rc;
+    for (int i = 1; i < nb_devices; i++) {
+        lvg_handle *q = nullptr;
+        rc = lvg_create(prob, devices[i], &q);
+        if (rc) {
+            const std::string e = g_create_error;
+            lvg_destroy(h);
+            return fail(nullptr, rc, "device %d: %s", devices[i], e.c_str());
+        }
+        q->tune = h->tune;
+        h->peers.push_back(q);
+    }
+    *out = h;
+    return LVG_OK;
+}
+
+int lvg_create_multi(const lvg_problem *prob, unsigned device_mask, lvg_handle **out) {
+    g_create_error.clear();
+    std::vector<int> devs;
+    for (int d = 0; d < 32; d++)
+        if (device_mask & (1u << d)) devs.push_back(d);
+    if (devs.empty()) {
+        if (out) *out = nullptr;
+        return fail(nullptr, LVG_E_ARG, "device_mask is empty");
+    }
+    return lvg_create_devices(prob, (int)devs.size(), devs.data(), out);
+}
+
+int lvg_nb_devices(const lvg_handle *h) { return h ? 1 + (int)h->peers.size() : 0; }
 
 }  // extern "C"
 
@@ -1122,6 +1201,57 @@ int solve_host(lvg_handle *h, const lvg_layers *layers, double *pops, const lvg_
 
 }  // namespace
 
+namespace {
+
+// the layers [lo, hi) of `L` as a view (no copy)
+lvg_layers layer_block(const lvg_layers &L, int nb_comp, int lo, int hi) {
+    lvg_layers v = L;
+    v.nb_lay = hi - lo;
+    const double **f[10] = {&v.temp_n, &v.temp_el, &v.el_conc, &v.h_conc, &v.ph2_conc,
+                            &v.oh2_conc, &v.he_conc, &v.mol_conc, &v.vel_turb, &v.vel_grad};
+    for (auto p : f) if (*p) *p += lo;
+    if (v.dust_conc) v.dust_conc += (size_t)lo * nb_comp;
+    return v;
+}
+
+// Multi-device handle: part d of the batch on device d (this handle, then its peers), one host
+// thread per device (each handle is used by exactly one thread: the one-handle-per-thread rule
+// holds), each on its own stream. part(handle, d) returns an LVG code. Kernel time: the slowest
+// device's (the step of a strongly split batch); launches summed.
+template <class F>
+int run_split(lvg_handle *h, F part) {
+    const int G = 1 + (int)h->peers.size();
+    std::vector<lvg_handle *> hs(G);
+    hs[0] = h;
+    for (int d = 1; d < G; d++) hs[d] = h->peers[d - 1];
+    std::vector<int> rc(G, LVG_OK);
+    std::vector<std::thread> th;
+    for (int d = 1; d < G; d++) th.emplace_back([&, d] { rc[d] = part(hs[d], d); });
+    rc[0] = part(hs[0], 0);
+    for (auto &t : th) t.join();
+    double ms = 0.;
+    int launches = 0, kind = -1;
+    for (int d = 0; d < G; d++) {
+        if (rc[d]) {
+            if (d) fail(h, rc[d], "device %d: %s", hs[d]->device, hs[d]->err.c_str());
+            return rc[d];
+        }
+        double m = 0.;
+        int n = 0;
+        (void)lvg_last_kernel_time(hs[d], &m, &n);
+        ms = std::max(ms, m);
+        launches += n;
+        if (kind < 0 && n) kind = hs[d]->last_kernel;
+    }
+    h->last_ms = ms;
+    h->last_launches = launches;
+    h->last_kernel = kind;
+    h->last_coll = 0;
+    return LVG_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 int lvg_solve_layers(lvg_handle *h, const lvg_layers *layers, double *pops, const lvg_solve_opts *o,
@@ -1132,9 +1262,23 @@ int lvg_solve_layers(lvg_handle *h, const lvg_layers *layers, double *pops, cons
     if (rc) return rc;
     const int nl = layers->nb_lay;
     if (o->init == LVG_INIT_WARM_CHAIN) {
-        // the reference default (radiative_transfer.cpp:247-252): one chain over the cloud
+        // the reference default (radiative_transfer.cpp:247-252): one chain over the cloud,
+        // sequential by construction (the first device of a multi-device handle)
         const int off[2] = {0, nl};
         return solve_host(h, layers, pops, o, status, 1, off);
+    }
+    if (!h->peers.empty() && nl > 0) {
+        // independent layers: contiguous blocks, layer l on device floor(l G / nl) (lvg_shard_range),
+        // no exchange between devices
+        const int G = 1 + (int)h->peers.size(), N = h->N;
+        return run_split(h, [&](lvg_handle *q, int d) {
+            int lo, hi;
+            lvg_shard_range(nl, G, d, &lo, &hi);
+            q->last_ms = 0.; q->last_launches = 0; q->last_kernel = -1;
+            if (hi == lo) return LVG_OK;
+            const lvg_layers v = layer_block(*layers, h->nb_comp, lo, hi);
+            return solve_host(q, &v, pops + (size_t)lo * N, o, status ? status + lo : nullptr, 0, nullptr);
+        });
     }
     return solve_host(h, layers, pops, o, status, 0, nullptr);
 }
@@ -1147,6 +1291,21 @@ int lvg_solve_chains(lvg_handle *h, const lvg_layers *layers, int nb_chain, cons
     if (rc) return rc;
     if (o->init != LVG_INIT_WARM_CHAIN) return fail(h, LVG_E_ARG, "lvg_solve_chains needs init = LVG_INIT_WARM_CHAIN");
     if ((rc = check_chains(h, layers->nb_lay, nb_chain, chain_off))) return rc;
+    if (!h->peers.empty() && layers->nb_lay > 0) {
+        // whole clouds per device, contiguous and balanced by layer count (lvg_chain_shard)
+        const int G = 1 + (int)h->peers.size(), N = h->N;
+        return run_split(h, [&](lvg_handle *q, int d) {
+            int c_lo, c_hi;
+            lvg_chain_shard(nb_chain, chain_off, G, d, &c_lo, &c_hi);
+            q->last_ms = 0.; q->last_launches = 0; q->last_kernel = -1;
+            const int lo = chain_off[c_lo], hi = chain_off[c_hi];
+            if (hi == lo) return LVG_OK;
+            std::vector<int> off(chain_off + c_lo, chain_off + c_hi + 1);
+            for (int &x : off) x -= lo;
+            const lvg_layers v = layer_block(*layers, h->nb_comp, lo, hi);
+            return solve_host(q, &v, pops + (size_t)lo * N, o, status ? status + lo : nullptr, c_hi - c_lo, off.data());
+        });
+    }
     return solve_host(h, layers, pops, o, status, nb_chain, chain_off);
 }
 
@@ -1199,6 +1358,29 @@ int lvg_boundary_layer_populations(lvg_handle *h, const lvg_layers *layers, doub
     if (!layers || !pops_out) return fail(h, LVG_E_ARG, "bad arguments");
     const int nl = layers->nb_lay, N = h->N;
     if (nl == 0) return LVG_OK;
+    if (!h->peers.empty()) {
+        const int G = 1 + (int)h->peers.size();
+        std::vector<lvg_handle *> peers;
+        peers.swap(h->peers);          // each block runs on its device's handle alone
+        std::vector<lvg_handle *> hs(1, h);
+        hs.insert(hs.end(), peers.begin(), peers.end());
+        std::vector<int> rc(G, LVG_OK);
+        std::vector<std::thread> th;
+        auto part = [&](int d) {
+            int lo, hi;
+            lvg_shard_range(nl, G, d, &lo, &hi);
+            if (hi == lo) return;
+            const lvg_layers v = layer_block(*layers, h->nb_comp, lo, hi);
+            rc[d] = lvg_boundary_layer_populations(hs[d], &v, pops_out + (size_t)lo * N);
+        };
+        for (int d = 1; d < G; d++) th.emplace_back(part, d);
+        part(0);
+        for (auto &t : th) t.join();
+        h->peers.swap(peers);
+        for (int d = 0; d < G; d++)
+            if (rc[d]) return d ? fail(h, rc[d], "device %d: %s", hs[d]->device, hs[d]->err.c_str()) : rc[d];
+        return LVG_OK;
+    }
     HIPCHECK(h, hipSetDevice(h->device));
     settle(h, h->stream);
     int rc = upload_layers(h, layers);

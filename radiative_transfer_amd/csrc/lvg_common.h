@@ -18,19 +18,26 @@
 enum { PH_SETUP, PH_BOUNDARY, PH_LINES, PH_ASSEMBLE, PH_PANEL, PH_TRSM, PH_GEMM, PH_BACKSUB, PH_CTL,
        PH_LSETUP, PH_PAIRS, PH_BDIAG, PH_BLOAD, PH_CLK_MEMTIME, PH_CLK_REALTIME, PH_RSV,
        PH_T_FETCH, PH_T_SOLVE, PH_T_STAGE, PH_P_RED, PH_P_POST, PH_P_WB, PH_BS_DIAG, PH_BS_UPD, PH_BS_WAIT,
-       PH_N };
-__device__ unsigned long long lvg_phase_cycles[32];
+       PH_ITERLU, PH_ITER, PH_N };
+// 64 counters: [0, 32) as named above; in the 256/512-thread block kernels the phases timed
+// inside a boundary-layer LU land at +32 (lvg_ph_shift), so the LU sub-phases of the boundary
+// and of the iteration LUs are told apart (tools/phase_timers.py)
+constexpr int PH_SLOTS = 64;
+__device__ unsigned long long lvg_phase_cycles[PH_SLOTS];
 #define TSTAMP(v) unsigned long long v = __builtin_amdgcn_s_memtime()
 #define RSTAMP(v) unsigned long long v = __builtin_amdgcn_s_memrealtime()
 // sums kept in LDS (no global atomics inside the timed code: queued atomics would hold
 // up the vmcnt waits of later loads), flushed once per block
-__shared__ unsigned long long lvg_ph_lds[32];
+__shared__ unsigned long long lvg_ph_lds[PH_SLOTS];
+__shared__ int lvg_ph_shift;
 #define RACC(ph, v0) do { if (lvg_tid() == 0) { unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); \
     lvg_ph_lds[ph] += t_ - (v0); } } while (0)
 #define TACC(ph, v0) do { if (lvg_tid() == 0) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
     lvg_ph_lds[ph] += t_ - (v0); } } while (0)
-#define PH_INIT() do { if (lvg_tid() < 32) lvg_ph_lds[lvg_tid()] = 0; __syncthreads(); } while (0)
-#define PH_FLUSH() do { __syncthreads(); if (lvg_tid() < 32 && lvg_ph_lds[lvg_tid()]) \
+#define PH_INIT() do { if (lvg_tid() < PH_SLOTS) lvg_ph_lds[lvg_tid()] = 0; if (lvg_tid() == 0) lvg_ph_shift = 0; \
+    __syncthreads(); } while (0)
+#define PH_SHIFT(v) do { if (lvg_tid() == 0) lvg_ph_shift = (v); } while (0)
+#define PH_FLUSH() do { __syncthreads(); if (lvg_tid() < PH_SLOTS && lvg_ph_lds[lvg_tid()]) \
     atomicAdd(&lvg_phase_cycles[lvg_tid()], lvg_ph_lds[lvg_tid()]); } while (0)
 #else
 #define TSTAMP(v) do {} while (0)
@@ -38,6 +45,7 @@ __shared__ unsigned long long lvg_ph_lds[32];
 #define RSTAMP(v) do {} while (0)
 #define RACC(ph, v0) do {} while (0)
 #define PH_INIT() do {} while (0)
+#define PH_SHIFT(v) do {} while (0)
 #define PH_FLUSH() do {} while (0)
 #endif
 
@@ -60,7 +68,22 @@ __device__ __forceinline__ int lvg_tid() {
 // waits for ALL of the wave's outstanding memory and LDS operations (s_waitcnt vmcnt(0)
 // lgkmcnt(0)). Through a gp<T> pointer it emits global loads with counted vmcnt waits.
 template <class T> using gp = __attribute__((address_space(1))) T *;
+//
+// RULE: glb() only on pointers that always name HBM (A, K, li, BK / BE / B, line_idx, the tables).
+// Never on y / diag / pop / b: those are LDS arrays on some paths (the y-cache when the lines fit
+// YCAP), and a global load of an LDS offset reads an unmapped address (the round-5 fault of probes
+// vgB / vgC, profiles/r5/variants.txt item 13). The checked build (-DLVG_CHECKED_GLB, used by the
+// timer / variant builds and tools/build_checked.sh) traps on a shared or private pointer.
+#ifdef LVG_CHECKED_GLB
+template <class T> __device__ __forceinline__ gp<T> glb(T *p) {
+#if __HIP_DEVICE_COMPILE__
+    if (__builtin_amdgcn_is_shared((const void *)p) || __builtin_amdgcn_is_private((const void *)p)) __builtin_trap();
+#endif
+    return (gp<T>)p;
+}
+#else
 template <class T> __device__ __forceinline__ gp<T> glb(T *p) { return (gp<T>)p; }
+#endif
 // 16-byte vectors for loads and stores through gp pointers (builtin vector types: HIP's double2 /
 // int4 classes cannot be copied from an address-space-qualified object)
 typedef double vd2 __attribute__((ext_vector_type(2)));
@@ -517,15 +540,6 @@ __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlan
 __device__ __forceinline__ double uni(double v) {
     return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
                             __builtin_amdgcn_readfirstlane(__double2loint(v)));
-}
-__device__ __forceinline__ Ctl uni(const Ctl &c) {
-    Ctl u;
-    u.acceleration = uni(c.acceleration); u.accel_start = uni(c.accel_start); u.accel_period = uni(c.accel_period);
-    u.nb_prev = uni(c.nb_prev); u.max_iter = uni(c.max_iter); u.iter_nb = uni(c.iter_nb);
-    u.nb_after_accel = uni(c.nb_after_accel);
-    u.best_eq = uni(c.best_eq); u.eq_error = uni(c.eq_error); u.pop_error = uni(c.pop_error); u.rel_error = uni(c.rel_error);
-    u.hp = uni(c.hp); u.np = uni(c.np); u.hr = uni(c.hr); u.nr = uni(c.nr);
-    return u;
 }
 
 __device__ __forceinline__ double *ring(double *base, int head, int i, int N) {

@@ -59,7 +59,7 @@ namespace LVG_NS {
 // the phases of waves that work while wave 0 waits are counted too (sums over 4 waves)
 #undef TACC
 #define TACC(ph, v0) do { if ((lvg_tid() & 63) == 0) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-    atomicAdd(&lvg_ph_lds[ph], t_ - (v0)); } } while (0)
+    atomicAdd(&lvg_ph_lds[(ph) + lvg_ph_shift], t_ - (v0)); } } while (0)
 #endif
 
 constexpr int BT   = LVG_BIG ? 768 : LVG_WIDE ? 512 : 256;   // threads per workgroup
@@ -84,13 +84,6 @@ static_assert(TR * (BT / 8) >= NMAX && TR % 2 == 0, "the register tiles cover ev
 #define LVG_COLL_PU 4
 #endif
 constexpr int COLL_PU = LVG_COLL_PU;        // 16x16 pair tiles per batch of the in-kernel collision build
-
-// The driver state of solve_layer (iteration control, pass flags) goes through LDS around
-// each LU, so that none of it occupies registers while the LU runs.
-struct Drv {
-    Ctl C;
-    int boundary, iters, retry;
-};
 
 constexpr int EGRID_CAP = 256;   // escape grids copied to LDS (esc_nd + esc_ng doubles)
 #if LVG_BIG
@@ -151,7 +144,6 @@ struct Smem {
     int8_t tet[LVG_MAX_CLASSES], tgrp[LVG_MAX_CLASSES];
     double dust[LVG_MAX_DUST];
     int    layer, pidx;
-    Drv    drv;                 // solve_layer's driver state across the LU
 };
 
 // OCC workgroups per CU must fit the CU's LDS (gfx950: 160 KB; the layout above, the L11 of
@@ -1081,8 +1073,12 @@ __device__ __forceinline__ bool solve_layer(const LvgDevProblem &P, const LvgLau
             if (Bdg) { src.BK = Kl; src.BE = P.einst; src.BD = Bdg; }
         }
         for (int i = t; i < N; i += BT) sm.bvec[i] = (i == 0) ? 1. : 0.;
+        PH_SHIFT(boundary ? 32 : 0);
         __syncthreads();
+        TSTAMP(tlu0);
         const double eq = block_lu_solve(S.A, N, sm.bvec, sm, src, !boundary);
+        PH_SHIFT(0);
+        if (!boundary) TACC(PH_ITERLU, tlu0);
         if (boundary) {
             TACC(PH_BOUNDARY, tb0);
             for (int i = t; i < N; i += BT) { sm.pold[i] = sm.blog[i]; S.given[i] = sm.blog[i]; }
@@ -1098,6 +1094,7 @@ __device__ __forceinline__ bool solve_layer(const LvgDevProblem &P, const LvgLau
         for (int i = t; i < N; i += BT) sm.pnew[i] = sm.blog[i];
         __syncthreads();
         next_step_post(C, P, S, sm, eq);
+        TACC(PH_ITER, tb0);
         found = C.rel_error < Lc.min_error;
         if (C.iter_nb < C.max_iter && !found) continue;
         iters += C.iter_nb;
@@ -1398,9 +1395,9 @@ extern "C" hipError_t LVG_SYM(lvg_kernel_occupancy)(int *blocks_per_cu) {
 
 #ifdef LVG_PHASE_TIMERS
 extern "C" int LVG_SYM(lvg_debug_phase_cycles)(unsigned long long *out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(LVG_NS::lvg_phase_cycles), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(LVG_NS::lvg_phase_cycles), sizeof(unsigned long long) * LVG_NS::PH_SLOTS) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[32] = {0};
+        unsigned long long z[LVG_NS::PH_SLOTS] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(LVG_NS::lvg_phase_cycles), z, sizeof z) != hipSuccess) return -1;
     }
     return 0;

@@ -922,9 +922,9 @@ extern "C" size_t lvg_wave_static_lds(void) { return sizeof(lvg::WaveShared); }
 
 #ifdef LVG_PHASE_TIMERS
 extern "C" int lvg_debug_wave_phase_cycles(unsigned long long *out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lvg::lvg_phase_cycles), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lvg::lvg_phase_cycles), sizeof(unsigned long long) * lvg::PH_SLOTS) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[32] = {0};
+        unsigned long long z[lvg::PH_SLOTS] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(lvg::lvg_phase_cycles), z, sizeof z) != hipSuccess) return -1;
     }
     return 0;

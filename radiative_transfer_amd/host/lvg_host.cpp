@@ -224,7 +224,12 @@ void iteration_scheme_lvg::init_molecule_data(const energy_diagram *di, const ei
     }
     prob = {&mol, &coll, &du, &et, (ov1 && ov2) ? &o1 : nullptr, (ov1 && ov2) ? &o2 : nullptr};
     if (h) { lvg_destroy(h); h = nullptr; }
-    check(lvg_create(&prob, device, &h), nullptr, "lvg_create");
+    if (devices.size() > 1) {
+        check(lvg_create_devices(&prob, (int)devices.size(), devices.data(), &h), nullptr, "lvg_create_devices");
+        if (verbosity) std::cout << "LVG solver tables for " << di->mol_name << " are on " << devices.size() << " devices" << std::endl;
+        return;
+    }
+    check(lvg_create(&prob, devices.empty() ? device : devices[0], &h), nullptr, "lvg_create");
     if (verbosity) std::cout << "LVG solver tables for " << di->mol_name << " are on device " << device << std::endl;
 }
 

@@ -208,6 +208,15 @@ public:
 
     // builds the device tables (lvg_create); must be called again if the molecule changes
     virtual void init_molecule_data(const energy_diagram *, const einstein_coeff *, const collisional_transitions *);
+    // several GPUs of this process for the next init_molecule_data (lvg_create_devices / the
+    // device_mask of SURVEY 8b): calc_molecular_populations with independent (boundary-layer)
+    // starts then splits the cloud's layers over them, one block per device. Empty: `device` only.
+    void set_devices(const std::vector<int> &devs) { devices = devs; }
+    void set_device_mask(unsigned mask) {
+        devices.clear();
+        for (int d = 0; d < 32; d++) if (mask & (1u << d)) devices.push_back(d);
+    }
+    int nb_devices() const { return h ? lvg_nb_devices(h) : 0; }
     int get_vector_dim() const { return nb_mol_lev; }
 
     void set_parameters(double temp_n, double temp_e, double el_conc, double h_conc, double ph2_conc,
@@ -229,6 +238,7 @@ public:
 
 protected:
     int nb_mol_lev = 0, verbosity = 0, device = 0;
+    std::vector<int> devices;     // set_devices: more than one -> lvg_create_devices
     bool overlap = false;
     const dust_model *dust;
     const lvg_method_data *loss_func;

@@ -21,7 +21,8 @@ EXPORTS = ("lvg_abi_version", "lvg_solve_opts_default", "lvg_create", "lvg_destr
            "lvg_nb_lev", "lvg_solve_layers", "lvg_layer_soa_rows", "lvg_solve_layers_device",
            "lvg_debug_calc_new_pop", "lvg_boundary_layer_populations", "lvg_find_opts_default",
            "lvg_find_transitions", "lvg_lim_luminosity", "lvg_last_kernel_time", "lvg_solve_chains",
-           "lvg_solve_chains_device", "lvg_last_coll_time", "lvg_set_tuning", "lvg_last_kernel_kind")
+           "lvg_solve_chains_device", "lvg_last_coll_time", "lvg_set_tuning", "lvg_last_kernel_kind",
+           "lvg_create_multi", "lvg_create_devices", "lvg_nb_devices", "lvg_shard_range", "lvg_chain_shard")
 
 _lib = None
 
@@ -58,6 +59,11 @@ def load(path: str = LIB_PATH):
     L.lvg_set_tuning.argtypes = [vp, C.c_char_p]
     L.lvg_last_kernel_kind.argtypes = [vp, C.POINTER(C.c_int)]
     L.lvg_find_opts_default.argtypes = [vp]
+    L.lvg_create_multi.argtypes = [vp, C.c_uint, C.POINTER(vp)]
+    L.lvg_create_devices.argtypes = [vp, i, C.POINTER(C.c_int), C.POINTER(vp)]
+    L.lvg_nb_devices.argtypes = [vp]
+    L.lvg_shard_range.argtypes = [i, i, i, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.lvg_chain_shard.argtypes = [i, C.POINTER(C.c_int), i, i, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     ip = C.POINTER(C.c_int)
     L.lvg_lim_luminosity.argtypes = [vp, vp, vp, dp, i, ip, ip, i, dp, dp, dp, dp, dp, dp]
     L.lvg_find_transitions.argtypes = [vp, vp, vp, dp, vp, i, C.POINTER(C.c_int), vp, dp, dp, dp]
@@ -72,16 +78,27 @@ class LvgSolver:
     (energy_diagram, einstein_coeff, collisional_transitions, iteration_scheme_lvg).
     """
 
-    def __init__(self, problem: abi.Problem, device: int = 0):
+    def __init__(self, problem: abi.Problem, device: int = 0, devices=None, device_mask: int = 0):
+        """One device (lvg_create), or several in this process: `devices` (lvg_create_devices,
+        repeats allowed) or `device_mask` (lvg_create_multi)."""
         self.lib = load()
         self.problem = problem
         self.N = problem.mol.nb_lev
         self._cp = problem.to_c()
         h = C.c_void_p()
-        rc = self.lib.lvg_create(self._cp.ptr, device, C.byref(h))
+        if devices is not None:
+            d = np.ascontiguousarray(devices, dtype=np.int32)
+            rc = self.lib.lvg_create_devices(self._cp.ptr, len(d), d.ctypes.data_as(C.POINTER(C.c_int)), C.byref(h))
+        elif device_mask:
+            rc = self.lib.lvg_create_multi(self._cp.ptr, device_mask, C.byref(h))
+        else:
+            rc = self.lib.lvg_create(self._cp.ptr, device, C.byref(h))
         if rc != 0:
             raise LvgError(f"lvg_create failed ({rc}): {self.lib.lvg_last_error(None).decode()}")
         self.h = h
+
+    def nb_devices(self) -> int:
+        return self.lib.lvg_nb_devices(self.h)
 
     def close(self):
         if getattr(self, "h", None):

@@ -198,6 +198,23 @@ int main(int argc, char **argv) {
             expect_equal("lim_luminosity_lvg (lum)", lg.data(), lum.data(), nro);
         }
     }
+    // 5. the same cloud over several devices behind one scheme (set_devices: lvg_create_devices;
+    //    on a one-GPU box the device list repeats device 0, each block with its own stream)
+    {
+        iteration_scheme_lvg multi(&dust, &esc);
+        multi.set_devices({0, 0, 0});
+        multi.init_molecule_data(&di, &ei, &co);
+        std::vector<double> pm((size_t)cloud.nb_lay * N, 0.), po((size_t)cloud.nb_lay * N, 0.);
+        std::vector<lvg_layer_status> so(cloud.nb_lay);
+        const std::vector<int> bad = calc_molecular_populations(&cloud, &multi, &di, &ei, &co, pm.data(), N, true, 0,
+                                                                init_policy::boundary_layer);
+        lvg_solve_opts o;
+        lvg_solve_opts_default(&o);
+        oracle_solve_layers(&P, &lp.view, po.data(), &o, so.data(), 1);
+        std::printf("%-44s %d devices\n", "set_devices({0, 0, 0})", multi.nb_devices());
+        failures += multi.nb_devices() != 3;
+        expect_equal("calc_molecular_populations (3 devices)", pm.data(), po.data(), pm.size());
+    }
     std::printf(failures ? "FAILED\n" : "ALL EQUAL\n");
     return failures ? 1 : 0;
 }

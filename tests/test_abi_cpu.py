@@ -107,3 +107,46 @@ def test_valid_problem_without_device_fails_cleanly(lib):
     assert rc == -2 and msg
     with pytest.raises(native.LvgError):
         native.LvgSolver(P)
+
+
+def test_partition_rules_match_dist(lib):
+    """lvg_shard_range / lvg_chain_shard (the multi-device handle's split, no device) are
+    dist.shard_range / dist.chain_shard, the rules of the one-process-per-GPU path."""
+    from radiative_transfer_amd import dist
+    lo, hi = C.c_int(), C.c_int()
+    for n in (0, 1, 7, 512, 4096, 4097, 16384):
+        for g in (1, 2, 3, 4, 8):
+            for r in range(g):
+                assert lib.lvg_shard_range(n, g, r, C.byref(lo), C.byref(hi)) == 0
+                assert (lo.value, hi.value) == dist.shard_range(n, g, r)
+    assert lib.lvg_shard_range(4, 0, 0, C.byref(lo), C.byref(hi)) == -1
+    assert lib.lvg_shard_range(4, 2, 2, C.byref(lo), C.byref(hi)) == -1
+    rng = np.random.default_rng(6)
+    for trial in range(40):
+        lens = rng.integers(0, 9, size=int(rng.integers(1, 30)))
+        off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+        for g in (1, 2, 3, 8):
+            for r in range(g):
+                assert lib.lvg_chain_shard(len(off) - 1, off.ctypes.data_as(C.POINTER(C.c_int)), g, r,
+                                           C.byref(lo), C.byref(hi)) == 0
+                assert (lo.value, hi.value) == dist.chain_shard(off, g, r), (off, g, r)
+
+
+def test_multi_device_create_rejects_without_touching_a_device(lib):
+    P, _, _ = synth.make_problem("ph2o45_1024", nb_lay=1)
+    cp = P.to_c()
+    h = C.c_void_p()
+    assert lib.lvg_create_multi(cp.ptr, 0, C.byref(h)) == -1
+    assert "empty" in lib.lvg_last_error(None).decode() and not h.value
+    assert lib.lvg_create_devices(cp.ptr, 0, None, C.byref(h)) == -1
+    assert lib.lvg_nb_devices(None) == 0
+
+
+def test_rejects_null_table_arrays(lib):
+    """NULL arrays fail with LVG_E_ARG in validation (they used to reach memcmp / hipMemcpy)."""
+    P, _, _ = synth.make_problem("oh24_overlap_2048", nb_lay=1)
+    cp = P.to_c()
+    cp.ov[1].gratio = None
+    h = C.c_void_p()
+    assert lib.lvg_create(cp.ptr, 0, C.byref(h)) == -1
+    assert "overlap table arrays missing" in lib.lvg_last_error(None).decode()

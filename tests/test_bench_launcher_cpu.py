@@ -106,3 +106,17 @@ def test_launcher_deadline_kills_ranks():
                           "--no-cpu", "--launch-timeout", "3", "--stub-hang", "120", timeout=100)
     assert rc == 124 and not lines
     assert "killed" in err
+
+
+def test_process_group_at_world_one():
+    """--process-group builds the process group at world size 1 (gloo with the stub; RCCL on
+    the GPU, tests/test_gpu_rccl.py) and the line names its backend; without it, no group."""
+    rc, lines, err = _run("--stub", "--process-group", "--steps", "1", "--workload", "ph2o45_1024", "--layers", "8",
+                          "--no-cpu")
+    assert rc == 0, err
+    line = json.loads(lines[0])
+    assert line["backend"] == "gloo" and line["n_gpus"] == 1
+    assert line["config"]["layer_iterations_per_step"] == 3 * 8
+    rc, lines, err = _run("--stub", "--steps", "1", "--workload", "ph2o45_1024", "--layers", "8", "--no-cpu")
+    assert rc == 0, err
+    assert json.loads(lines[0])["backend"] is None

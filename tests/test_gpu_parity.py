@@ -116,12 +116,13 @@ def test_empty_and_error_paths():
 
 # ---- full BASELINE sizes ---------------------------------------------------------------
 
-@pytest.mark.parametrize("name,exact_all", [("ph2o45_1024", True), ("oh24_overlap_2048", True),
-                                            ("ch3oha256_4096", False), ("ch3ohe256_sweep", False)])
-def test_full_size(name, exact_all):
-    """Every layer converges, populations are normalised and non-negative, results are
-    identical run to run; bit-exact against the oracle on all layers (small N) or on a
-    spread subset (N = 256, where the oracle would take minutes)."""
+@pytest.mark.parametrize("name", ["ph2o45_1024", "oh24_overlap_2048", "ch3oha256_4096", "ch3ohe256_sweep"])
+def test_full_size(name):
+    """The four BASELINE configurations at full size (1024 / 2048 / 4096 layers, 16,384
+    sweep cells): every layer converges, populations are normalised and non-negative,
+    results are identical run to run, and EVERY layer is bit-exact against the oracle
+    (the oracle runs on the box's OpenMP threads: 4096 CH3OH-A layers in ~2 s on 16,
+    the 16,384 CH3OH-E cells in ~8 s)."""
     s, P, L, o = solver_for(name)
     opts = abi.default_opts(**o)
     p1, s1 = s.solve_layers(L, opts)
@@ -130,6 +131,5 @@ def test_full_size(name, exact_all):
     assert np.all(s1["converged"] == 1)
     assert np.all(np.abs(p1.sum(axis=1) - 1.0) < 1e-9)
     assert p1.min() > -1e-12
-    idx = np.arange(L.nb_lay) if exact_all else np.unique(np.linspace(0, L.nb_lay - 1, 16).astype(int))
-    po, so = oracle.solve_layers(P, L.subset(idx), opts)
-    assert_same(p1[idx], s1[idx], po, so)
+    po, so = oracle.solve_layers(P, L, opts)
+    assert_same(p1, s1, po, so)

@@ -11,19 +11,19 @@ opts = abi.default_opts(**o)
 s = native.LvgSolver(P)
 lib = native.load()
 # the wave kernel (N <= 64) keeps its counters in its own translation unit (lvg_wave.hip)
-buf = (C.c_ulonglong * 32)()
+buf = (C.c_ulonglong * 64)()
 
 
 def read(out, reset):
     """The counters of every kernel that may have run, summed (one kind runs per launch)."""
     fns = [lib.lvg_debug_wave_phase_cycles] if P.mol.nb_lev <= 64 else \
           [lib.lvg_debug_phase_cycles, lib.lvg_debug_phase_cycles_wide]
-    tot = [0] * 32
+    tot = [0] * 64
     for f in fns:
-        b = (C.c_ulonglong * 32)()
+        b = (C.c_ulonglong * 64)()
         f(b, reset)
         tot = [x + y for x, y in zip(tot, b)]
-    for i in range(32):
+    for i in range(64):
         out[i] = tot[i]
 
 _, st = s.solve_layers(L, opts)

@@ -19,15 +19,16 @@ nl = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
 P, L, o = synth.make_problem(name, nb_lay=nl)
 s = native.LvgSolver(P)
 lib = native.load()
-buf = (C.c_ulonglong * 32)()
+NS = 64                      # counters per kernel (PH_SLOTS): boundary-LU sub-phases at +32
+buf = (C.c_ulonglong * NS)()
 
 
 def read_counters(out, reset):
     """256- and 512-thread kernels' counters summed (one kind runs per launch)."""
-    a, b = (C.c_ulonglong * 32)(), (C.c_ulonglong * 32)()
+    a, b = (C.c_ulonglong * NS)(), (C.c_ulonglong * NS)()
     lib.lvg_debug_phase_cycles(a, reset)
     lib.lvg_debug_phase_cycles_wide(b, reset)
-    for i in range(32):
+    for i in range(NS):
         out[i] = a[i] + b[i]
 
 
@@ -36,13 +37,34 @@ read_counters(buf, 1)
 t = time.time(); pops, st = s.solve_layers(L, abi.default_opts(**o)); dt = time.time() - t
 ms, _ = s.last_kernel_time()
 read_counters(buf, 1)
-cyc = np.array(buf[:32], dtype=np.float64)
+cyc = np.array(buf[:NS], dtype=np.float64)
 clk = np.array(buf[13:15], dtype=np.float64)
 its = st["iterations"].sum()
 print(f"{name} layers={nl} kernel {ms:.2f} ms, iterations {its}, LUs {its + nl}")
-tot = cyc[:9].sum() - cyc[1]   # boundary LU overlaps the LU phases
-for i in SHOW:
-    n, c = names[i], cyc[i]
-    print(f"  {n:16s} {c/1e6:10.2f} Mcyc  {100*c/tot:5.1f}%   per-LU {c/(its+nl):10.0f} cyc   per-layer {c/nl:10.0f} cyc")
+tot = cyc[13]                 # wave-cycles: every wave's memtime over its solve_layer calls
+if cyc[26] > 0:
+    # the honest split (round 6): wall wave-cycles of each part over the total wave-cycles
+    rows = [("setup + collision build (per layer)", cyc[0], nl),
+            ("boundary LU (per layer)", cyc[1], nl),
+            ("iteration, all of it (per iteration)", cyc[26], its),
+            ("  of which the iteration LU", cyc[25], its),
+            ("  of which line terms", cyc[2], its),
+            ("  of which column diagonals", cyc[3], its)]
+    print(f"  total {tot/1e6:.1f} M wave-cycles (memtime summed over waves)")
+    for n, c, u in rows:
+        print(f"  {n:40s} {c/1e6:10.2f} Mcyc  {100*c/tot:5.1f}%   per unit {c/max(u,1):10.0f} cyc")
+    print(f"  boundary LU / iteration LU (per LU, wall wave-cycles): {cyc[1]/nl / max(cyc[25]/max(its,1), 1):.3f}")
+    print("  LU sub-phases per LU, iteration | boundary:")
+    for i in SHOW:
+        if i in (0, 1, 2, 3, 8, 9, 10, 11, 13, 14):
+            continue
+        n = names[i]
+        ci, cb = cyc[i], cyc[i + 32]
+        print(f"    {n:24s} {ci/max(its,1):10.0f} | {cb/max(nl,1):10.0f} cyc")
+else:
+    tot = cyc[:9].sum() - cyc[1]   # boundary LU overlaps the LU phases
+    for i in SHOW:
+        n, c = names[i], cyc[i]
+        print(f"  {n:16s} {c/1e6:10.2f} Mcyc  {100*c/tot:5.1f}%   per-LU {c/(its+nl):10.0f} cyc   per-layer {c/nl:10.0f} cyc")
 print(f"  in-kernel clock (sum memtime / sum realtime x 100 MHz): {clk[0] / max(clk[1], 1) * 0.1:.3f} GHz; busy WG-time {clk[1] / 1e8:.3f} s")
 np.savez(f"/root/repo/gpurun_out/dump_{name}_{nl}.npz", pops=pops, iters=st["iterations"], conv=st["converged"])
