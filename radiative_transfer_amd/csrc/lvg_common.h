@@ -113,8 +113,11 @@ __device__ __forceinline__ double wave_max(double v) {
 template <int CTRL, int ROW, int BANK>
 __device__ __forceinline__ double dpp_d(double x) {
     int lo = __double2loint(x), hi = __double2hiint(x);
-    lo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROW, BANK, false);
-    hi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROW, BANK, false);
+    // every caller broadcasts within full rows (row_newbcast, all rows and banks): no lane keeps
+    // an old value, so the DPP move writes a fresh register instead of a copy of x
+    static_assert(ROW == 0xf && BANK == 0xf, "mov_dpp leaves disabled lanes undefined");
+    lo = __builtin_amdgcn_mov_dpp(lo, CTRL, ROW, BANK, false);
+    hi = __builtin_amdgcn_mov_dpp(hi, CTRL, ROW, BANK, false);
     return __hiloint2double(hi, lo);
 }
 template <int CTRL, int ROW, int BANK>

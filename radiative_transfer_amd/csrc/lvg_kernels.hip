@@ -298,6 +298,7 @@ struct LuSrc {
     // unfused, boundary matrix formed from the layer's K (no electron rates): row 0 = 1,
     // diagonal BD, above it 0.5 A_{d,r} + K_{r,d} (BE = einst), below it K_{r,d}
     const double *BK = nullptr, *BE = nullptr, *BD = nullptr;
+    const double *BET = nullptr;   // einst transposed (einst_t): einst[d][r] at BET[r * N + d]
 };
 
 // ---- back substitution U x = y in logical order, blocked by NB from the bottom:
@@ -1070,7 +1071,7 @@ __device__ __forceinline__ bool solve_layer(const LvgDevProblem &P, const LvgLau
             src.K = Kl; src.y = yp; src.li = M.line_idx; src.pop = sm.pold; src.df = S.df;
         } else {
             src.B = Bsrc;
-            if (Bdg) { src.BK = Kl; src.BE = P.einst; src.BD = Bdg; }
+            if (Bdg) { src.BK = Kl; src.BE = P.einst; src.BET = P.einst_t; src.BD = Bdg; }
         }
         for (int i = t; i < N; i += BT) sm.bvec[i] = (i == 0) ? 1. : 0.;
         PH_SHIFT(boundary ? 32 : 0);

@@ -206,9 +206,13 @@ __device__ __forceinline__ void lu_apply(double (&acc)[S4][CW], const int (&prow
             for (int i = 0; i < CL; i++) x[i] = Ub[r][CL * q4 + i];
         }
         const double *lrw = sm.pu.L11c[ci][r < CW ? r : 0];
+        // the lane's L11 row read once, ahead of the steps (one LDS wait instead of one per step)
+        double lmv[CW - 1];
+#pragma unroll
+        for (int m = 0; m < CW - 1; m++) lmv[m] = lrw[m];
 #define LVG_TRSM_STEP(M_)                                                                  \
         if ((M_) < nb - 1) {                                                               \
-            const double lm = lrw[M_];                                                     \
+            const double lm = lmv[M_];                                                     \
             _Pragma("unroll") for (int i = 0; i < CL; i++) {                               \
                 const double y = dpp_d<0x150 + (M_), 0xf, 0xf>(x[i]);                      \
                 if (r > (M_)) x[i] = fma(-lm, y, x[i]);                                    \
@@ -365,10 +369,21 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
                     for (int jj = 0; jj < CW; jj++) kv[jj] = rsrc[(int64_t)pr * N + min(c0 + jj, N - 1)];
                 }
                 if (src.BK) {
+                    // einst[d][pr] for the chunk's columns d: row pr of the transposed copy, as the K row
+                    double ev[CW];
+                    if (nw == CW) {
+                        gp<const vd2u> e2 = reinterpret_cast<gp<const vd2u>>(
+                            okr ? glb(src.BET) + (int64_t)pr * N + c0 : glb((const double *)lu_zero_row));
+#pragma unroll
+                        for (int jj = 0; jj < CW / 2; jj++) { const vd2u x = e2[jj]; ev[2 * jj] = x.x; ev[2 * jj + 1] = x.y; }
+                    } else {
+#pragma unroll
+                        for (int jj = 0; jj < CW; jj++) ev[jj] = glb(src.BET)[(int64_t)pr * N + min(c0 + jj, N - 1)];
+                    }
 #pragma unroll
                     for (int jj = 0; jj < CW; jj++) {
                         const int d = c0 + jj, dc = min(d, N - 1);
-                        const double e = glb(src.BE)[(int64_t)dc * N + pr];
+                        const double e = ev[jj];
                         const double dg = src.BD[dc];
                         double v = (pr < d) ? 0.5 * e + kv[jj] : kv[jj];   // build_collision_operators: 0.5 * af + dn
                         if (pr == d) v = dg;
