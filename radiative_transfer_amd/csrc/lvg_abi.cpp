@@ -344,6 +344,8 @@ int compile_rule(lvg_handle *h, const lvg_problem *prob, std::vector<uint8_t> &p
         for (int k = 0; k < tl.nt; k++) { tt.table[kv.second][k] = (int8_t)tl.table[k]; tt.combo[kv.second][k] = (int8_t)tl.combo[k]; }
         tt.etable[kv.second] = (int8_t)tl.etable;
         tt.group[kv.second] = (int8_t)tl.group;
+        tt.nt_max = std::max(tt.nt_max, tl.nt);
+        if (tl.etable >= 0) tt.any_e = 1;
     }
     tt.nb_combos = (int)cb.w.size();
     for (size_t i = 0; i < cb.w.size(); i++)

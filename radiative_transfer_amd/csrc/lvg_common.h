@@ -451,6 +451,105 @@ __device__ __forceinline__ void build_collision_operators(const LvgDevProblem &P
     TACC(PH_BDIAG, tq1);
 }
 
+// build_collision_operators with two batches in flight (the block kernels, no B: the boundary
+// matrix is formed from K in the LU's chunk load). NT neutral term slots and, when HE, the
+// electron slot are loaded for every pair, UNCONDITIONALLY (a missing term reads a clamped address
+// of table 0 and is never used), and the K stores are unconditional too (an idle lane writes
+// K[0], a diagonal entry nothing reads), so the number of memory operations between a batch's
+// loads and their use is fixed and the waits are counted: batch b + 1's loads are issued
+// before batch b is evaluated. Same operations per pair as build_collision_operators.
+template <int BTH, int PU, int NT, bool HE, class SM>
+__device__ __forceinline__ void build_collision_pipe(const LvgDevProblem &P, SM &sm, double *K, const uint8_t *cls_gen,
+                                                     bool electrons) {
+    typedef __attribute__((address_space(3))) const uint8_t *lds_u8;
+    const lds_u8 cls_lds = (lds_u8)cls_gen;          // the pair classes staged in LDS (required)
+    const int N = P.N, t = lvg_tid();
+    const double T = sm.T, Te = sm.Te;
+    const int nt = (N + 15) >> 4, ntiles = nt * (nt + 1) / 2;
+    const int fl = (t >> 4) & 15, sl = t & 15;
+    constexpr int TG = BTH / 256;
+    constexpr int NS = NT + (HE ? 1 : 0);
+    const int tg = t >> 8;
+    gp<double> Kg = glb(K);
+    struct Stage {
+        int pc[PU], fc[PU], sc[PU], cls[PU];
+        double ef[PU], es[PU], gf[PU], gs[PU];
+        double c0[PU][NS], c1[PU][NS];
+    };
+    auto issue = [&](Stage &S, int q0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < PU; u++) {
+            const int q = q0 + tg * PU + u;
+            int F = (int)((sqrt(8. * q + 1.) - 1.) * 0.5);
+            while (F * (F + 1) / 2 > q) F--;
+            while ((F + 1) * (F + 2) / 2 <= q) F++;
+            const int S2 = q - F * (F + 1) / 2;
+            S.fc[u] = 16 * F + fl; S.sc[u] = 16 * S2 + sl;
+            S.pc[u] = (q < ntiles && S.fc[u] < N && S.sc[u] < S.fc[u]) ? S.fc[u] * (S.fc[u] - 1) / 2 + S.sc[u] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < PU; u++) S.cls[u] = cls_lds[S.pc[u] < 0 ? 0 : S.pc[u]];
+#pragma unroll
+        for (int u = 0; u < PU; u++) {
+            const bool ok = S.pc[u] >= 0;
+            const int f = ok ? S.fc[u] : 1, s = ok ? S.sc[u] : 0;
+            S.ef[u] = glb(P.energy)[f]; S.es[u] = glb(P.energy)[s];
+            S.gf[u] = glb(P.g)[f]; S.gs[u] = glb(P.g)[s];
+#pragma unroll
+            for (int k = 0; k < NS; k++) {
+                int tb = (k < NT) ? sm.ttab[S.cls[u]][k] : sm.tet[S.cls[u]];
+                tb = tb < 0 ? 0 : tb;
+                const int64_t pcc = S.pc[u] < 0 ? 0 : S.pc[u] < sm.timax[tb] ? S.pc[u] : sm.timax[tb] - 1;
+                S.c0[u][k] = glb(sm.tcol[tb])[pcc];
+                S.c1[u][k] = glb(sm.tder[tb])[pcc];      // slope (calc_coeff_deriv)
+            }
+        }
+    };
+    auto eval_store = [&](const Stage &S) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < PU; u++) {
+            const int cl = S.cls[u], f = S.fc[u], s = S.sc[u];
+            const int grp = sm.tgrp[cl];
+            double dn = 0., gsum = 0.;
+            int ng = 0;
+#pragma unroll
+            for (int k = 0; k < NT; k++) {
+                const int tb = sm.ttab[cl][k];
+                if (tb < 0) break;
+                const double r = (S.c0[u][k] + S.c1[u][k] * sm.tx[tb]) * sm.cc[sm.tcombo[cl][k]];   // get_rate
+                if (k < grp) dn = (k == 0) ? r : dn + r;
+                else { gsum = (ng == 0) ? r : gsum + r; ng++; }
+            }
+            if (ng) dn = dn + gsum;
+            const double de = S.es[u] - S.ef[u];
+            double un = 0.;
+            if (dn > MIN_COLLISION_RATE) un = dn * lvg_exp(de * CM_INVERSE_TO_KELVINS / T) * S.gf[u] / S.gs[u];
+            else dn = 0.;
+            double dE = 0., uE = 0.;
+            if (HE) {
+                const int et = sm.tet[cl];
+                if (et >= 0 && electrons) {
+                    dE = (S.c0[u][NS - 1] + S.c1[u][NS - 1] * sm.tx[et]) * sm.ne;
+                    if (dE > MIN_COLLISION_RATE) uE = dE * lvg_exp(de * CM_INVERSE_TO_KELVINS / Te) * S.gf[u] / S.gs[u];
+                    else dE = 0.;
+                }
+            }
+            const bool ok = S.pc[u] >= 0;
+            Kg[ok ? (int64_t)s * N + f : 0] = dn + dE;
+            Kg[ok ? (int64_t)f * N + s : 0] = un + uE;
+        }
+    };
+    Stage A, B;
+    constexpr int STEP = PU * TG;
+    issue(A, 0);
+    for (int q0 = 0; q0 < ntiles; q0 += 2 * STEP) {
+        issue(B, q0 + STEP);
+        eval_store(A);
+        if (q0 + 2 * STEP < ntiles) issue(A, q0 + 2 * STEP);
+        if (q0 + STEP < ntiles) eval_store(B);
+    }
+}
+
 // ------------------------------------------------------------------------------
 // radiative terms: intensity_calc (iteration_lvg.cpp:163-185, :428-501)
 // ------------------------------------------------------------------------------

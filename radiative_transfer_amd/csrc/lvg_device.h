@@ -32,6 +32,8 @@ struct LvgTermTable {
                                                    // (coll_rates_oh.cpp:341: d += k1*c1 + k2*c2)
     double combo_w[LVG_MAX_COMBOS][5];             // combo = sum_s w[s] * n[s] (he, ph2, oh2, h, e)
     int    nb_combos;
+    int    nt_max;                                 // most neutral terms of any class
+    int    any_e;                                  // some class has an electron table
 };
 
 struct LvgModeLines {          // one radiative scheme (plain LVG or line overlap)

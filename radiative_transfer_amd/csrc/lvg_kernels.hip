@@ -84,6 +84,9 @@ static_assert(TR * (BT / 8) >= NMAX && TR % 2 == 0, "the register tiles cover ev
 #define LVG_COLL_PU 4
 #endif
 constexpr int COLL_PU = LVG_COLL_PU;        // 16x16 pair tiles per batch of the in-kernel collision build
+#ifndef LVG_COLLP_PU
+#define LVG_COLLP_PU 2     // ... and per batch of the pipelined build (two batches in flight)
+#endif
 
 constexpr int EGRID_CAP = 256;   // escape grids copied to LDS (esc_nd + esc_ng doubles)
 #if LVG_BIG
@@ -175,6 +178,27 @@ __device__ __forceinline__ void layer_collisions(const LvgDevProblem &P, Smem &s
                                                  bool electrons = true) {
     const int M = P.N * (P.N - 1) / 2;
     uint8_t *cls = M <= (int)sizeof(sm.pu) ? reinterpret_cast<uint8_t *>(&sm.pu) : nullptr;
+    // no boundary matrix to write and at most three neutral terms per pair (CH3OH, OH, p-H2O
+    // below 3 tables): the pipelined build, two batches in flight (+1.8%, profiles/r6/variants.txt
+    // item 2; not in the 768-thread kernel, whose register allocation it wrecks); otherwise
+    // build_collision_operators
+#if !LVG_BIG
+    if (!B && cls && P.terms.nt_max <= 3) {
+        TSTAMP(tq0);
+        {
+            const int n16 = M >> 4;
+            const uint4 *src4 = reinterpret_cast<const uint4 *>(P.pair_class);
+            for (int e = lvg_tid(); e < n16; e += BT) reinterpret_cast<uint4 *>(cls)[e] = src4[e];
+            for (int e = (n16 << 4) + lvg_tid(); e < M; e += BT) cls[e] = P.pair_class[e];
+            __syncthreads();
+        }
+        if (electrons && P.terms.any_e) build_collision_pipe<BT, LVG_COLLP_PU, 3, true>(P, sm, K, cls, true);
+        else build_collision_pipe<BT, LVG_COLLP_PU, 3, false>(P, sm, K, cls, false);
+        __syncthreads();
+        TACC(PH_PAIRS, tq0);
+        return;
+    }
+#endif
     build_collision_operators<BT, COLL_PU>(P, sm, K, B, cls, electrons);
 }
 

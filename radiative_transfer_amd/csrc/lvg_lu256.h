@@ -380,11 +380,20 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
 #pragma unroll
                         for (int jj = 0; jj < CW; jj++) ev[jj] = glb(src.BET)[(int64_t)pr * N + min(c0 + jj, N - 1)];
                     }
+                    double bd[CW];
+                    if (src.BD == sm.diag) {     // B's diagonal in LDS (formed in-kernel) or HBM (coll_kernel)
+                        typedef __attribute__((address_space(3))) const double *lds_d;
+#pragma unroll
+                        for (int jj = 0; jj < CW; jj++) bd[jj] = ((lds_d)src.BD)[min(c0 + jj, N - 1)];
+                    } else {
+#pragma unroll
+                        for (int jj = 0; jj < CW; jj++) bd[jj] = glb(src.BD)[min(c0 + jj, N - 1)];
+                    }
 #pragma unroll
                     for (int jj = 0; jj < CW; jj++) {
-                        const int d = c0 + jj, dc = min(d, N - 1);
+                        const int d = c0 + jj;
                         const double e = ev[jj];
-                        const double dg = src.BD[dc];
+                        const double dg = bd[jj];
                         double v = (pr < d) ? 0.5 * e + kv[jj] : kv[jj];   // build_collision_operators: 0.5 * af + dn
                         if (pr == d) v = dg;
                         if (pr == 0) v = 1.;
@@ -394,34 +403,47 @@ __device__ __forceinline__ double block_lu_solve(double *A, int N, double *b, Sm
 #pragma unroll
                 for (int jj = 0; jj < CW; jj++) acc[s][jj] = (okr && jj < nw) ? kv[jj] : 0.;
             } else {
+                // every load unconditional through global (K, line index) or LDS-typed (y-cache)
+                // pointers, rows past N reading row 0 and columns past N column N - 1, the line
+                // terms gathered at clamped indices: the values are selected after
                 int li[CW];
+                double kv[CW], yv[CW];
                 const int64_t o = (int64_t)(okr ? pr : 0) * N + c0;
+                const gp<const double> Kg = glb(src.K) + o;
+                const gp<const int> Lg = glb(src.li) + o;
                 if ((N & 3) == 0 && nw == CW) {
-                    const double2 *k2 = reinterpret_cast<const double2 *>(src.K + o);
-                    const int4 *l4 = reinterpret_cast<const int4 *>(src.li + o);
+                    const gp<const vd2> k2 = reinterpret_cast<gp<const vd2>>(Kg);
+                    const gp<const vi4> l4 = reinterpret_cast<gp<const vi4>>(Lg);
 #pragma unroll
-                    for (int jj = 0; jj < CW / 2; jj++) {
-                        const double2 v = okr ? k2[jj] : make_double2(0., 0.);
-                        acc[s][2 * jj] = v.x; acc[s][2 * jj + 1] = v.y;
-                    }
+                    for (int jj = 0; jj < CW / 2; jj++) { const vd2 x = k2[jj]; kv[2 * jj] = x.x; kv[2 * jj + 1] = x.y; }
 #pragma unroll
                     for (int jj = 0; jj < CW / 4; jj++) {
-                        const int4 v = okr ? l4[jj] : make_int4(-1, -1, -1, -1);
-                        li[4 * jj] = v.x; li[4 * jj + 1] = v.y; li[4 * jj + 2] = v.z; li[4 * jj + 3] = v.w;
+                        const vi4 x = l4[jj];
+                        li[4 * jj] = x.x; li[4 * jj + 1] = x.y; li[4 * jj + 2] = x.z; li[4 * jj + 3] = x.w;
                     }
                 } else {
 #pragma unroll
                     for (int jj = 0; jj < CW; jj++) {
-                        const bool ok = okr && jj < nw;
-                        acc[s][jj] = ok ? src.K[o + jj] : 0.;
-                        li[jj] = ok ? src.li[o + jj] : -1;
+                        const int cj = min(jj, N - 1 - c0);
+                        kv[jj] = Kg[cj];
+                        li[jj] = Lg[cj];
                     }
+                }
+                if (src.y == sm.ylds) {
+                    typedef __attribute__((address_space(3))) const double *lds_y;
+                    const lds_y Yl = (lds_y)src.y;
+#pragma unroll
+                    for (int jj = 0; jj < CW; jj++) yv[jj] = Yl[li[jj] >= 0 ? li[jj] : 0];
+                } else {
+                    const gp<const double> Yg = glb(src.y);
+#pragma unroll
+                    for (int jj = 0; jj < CW; jj++) yv[jj] = Yg[li[jj] >= 0 ? li[jj] : 0];
                 }
 #pragma unroll
                 for (int jj = 0; jj < CW; jj++) {
                     const int d = c0 + jj;
-                    double v = acc[s][jj];
-                    if (li[jj] >= 0) v = v + src.y[li[jj]];
+                    double v = kv[jj];
+                    v = (okr && li[jj] >= 0) ? v + yv[jj] : v;
                     if (pr == d) v = sm.diag[d < NMAX ? d : 0];
                     if (pr == 0) v = 1.;
                     acc[s][jj] = (okr && jj < nw) ? v : 0.;
