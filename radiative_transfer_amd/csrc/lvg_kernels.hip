@@ -168,19 +168,7 @@ __device__ __forceinline__ double block_max(double v, Smem &sm) {
 }
 
 __device__ __forceinline__ void layer_setup(const LvgDevProblem &P, const LvgLaunch &Lc, int l, Smem &sm) {
-#if LVG_V_LSET
-    // the collision tables' temperature bisections by lanes of wave 1, one table each, beside thread
-    // 0's scalars (wave 0): the dependent grid loads of the tables overlap instead of running in turn
-    const int t = lvg_tid();
-    if (t == 0) layer_scalars(P, Lc, l, sm, false);
-    else if (t >= 64 && t - 64 < P.nb_tables) {
-        const double *s = Lc.soa + Lc.lay_offset + l;
-        const double T = s[0], Te = s[(int64_t)Lc.soa_ld];
-        layer_table(P, t - 64, T, Te, sm);
-    }
-#else
     if (lvg_tid() == 0) layer_scalars(P, Lc, l, sm);
-#endif
     __syncthreads();
 }
 
@@ -353,24 +341,6 @@ __device__ __forceinline__ void back_substitute(const double *A, int N, const do
     auto load_blk = [&](int kb, double &dv, double (&u)[NB]) {
         const int k0 = kb * NB, nb = min(NB, N - k0);
         const int r = t / NB, c = t - r * NB;
-#if LVG_V_BSG2
-        // global (not flat) loads issued by every thread at clamped indices, the values kept raw:
-        // the diagonal entry is only stored for r, c < nb and the U segment only used for t < k0
-        {
-            const gp<const double> Ag = glb(A);
-            dv = Ag[(int64_t)sm.perm[k0 + min(r, nb - 1)] * N + k0 + min(c, nb - 1)];
-            const gp<const double> row = Ag + (int64_t)sm.perm[t < k0 ? t : 0] * N + k0;
-            if ((N & 1) == 0 && nb == NB) {
-                const gp<const vd2> r2 = reinterpret_cast<gp<const vd2>>(row);
-#pragma unroll
-                for (int m = 0; m < NB / 2; m++) { const vd2 v = r2[m]; u[2 * m] = v.x; u[2 * m + 1] = v.y; }
-            } else {
-#pragma unroll
-                for (int m = 0; m < NB; m++) u[m] = row[min(m, nb - 1)];
-            }
-            return;
-        }
-#endif
         dv = (r < nb && c < nb) ? A[(int64_t)sm.perm[k0 + r] * N + k0 + c] : 0.;
         const double *row = A + (int64_t)sm.perm[t < k0 ? t : 0] * N + k0;
         if ((N & 1) == 0 && nb == NB) {
