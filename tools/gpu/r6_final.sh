@@ -27,7 +27,7 @@ for G in 2 4 8; do
   tail -1 $OUT/shard$G.txt
 done
 if [ -z "$NOTIMERS" ]; then
-  timeout -k 10 300 python tools/phase_timers.py ch3oha256_4096 4096 > $OUT/phase_4096.txt 2>&1 || exit 4
+  timeout -k 10 300 python tools/phase_timers.py --v2 ch3oha256_4096 4096 > $OUT/phase_4096.txt 2>&1 || exit 4
   sed -n 1,12p $OUT/phase_4096.txt
   for wl in ph2o45_1024 oh24_overlap_2048; do
     timeout -k 10 300 python tools/latency_timers.py $wl > $OUT/wave_$wl.txt 2>&1 || exit 5
