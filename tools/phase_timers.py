@@ -13,7 +13,8 @@ if "--v2" in sys.argv:          # the N <= 256 kernel's column-owned LU (lvg_lu2
     names[4], names[5], names[6] = "LU panel (owner)", "LU step-end barrier", "LU rank-16 updates"
     names[12], names[15], names[16], names[17], names[21] = "LU block load", "LU residual (4 bar)", \
         " (L fetch+stage+bar)", " (TRSM, U rows)", " (publish + 2 bar)"
-    SHOW = list(range(13)) + [15, 16, 17, 21]
+    names += [" (backsub: diag solve)", " (backsub: row updates)", " (wait before backsub)"]
+    SHOW = list(range(13)) + [15, 16, 17, 21, 22, 23, 24]
 name = sys.argv[1] if len(sys.argv) > 1 else "ch3oha256_4096"
 nl = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
 P, L, o = synth.make_problem(name, nb_lay=nl)
