@@ -121,6 +121,30 @@ def _generic_problem():
     return P, L, o
 
 
+@pytest.mark.parametrize("kind", BLOCK_KINDS)
+def test_pipelined_collision_build_with_electrons(kind):
+    """The block kernels' pipelined collision build (build_collision_pipe: no boundary matrix
+    written, at most three neutral terms) with its electron slot: the GENERIC rule's electron
+    tables (coll_rates.cpp:181-217) on layers started from given populations and on warm
+    chains, where no boundary matrix is built. Bit-exact against the oracle."""
+    P, L, o = _generic_problem()
+    s = LvgSolver(P)
+    s.set_tuning(_block_tuning(kind))
+    p0, _ = oracle.solve_layers(P, L, abi.default_opts(**o))
+    guess = 0.5 * p0 + 0.5 / P.mol.nb_lev
+    _cmp(s, P, L, abi.default_opts(init=abi.LVG_INIT_GIVEN, **o), pops=guess)
+    assert s.last_kernel_kind() == kind
+    _cmp(s, P, L, abi.default_opts(init=abi.LVG_INIT_WARM_CHAIN, **o))
+    assert s.last_kernel_kind() == kind
+    off = np.array([0, 3, 8], dtype=np.int32)
+    wopts = abi.default_opts(init=abi.LVG_INIT_WARM_CHAIN, **o)
+    pg, sg = s.solve_chains(L, off, wopts)
+    po, so = oracle.solve_chains(P, L, off, wopts)
+    assert_same(pg, sg, po, so)
+    assert s.last_kernel_kind() == kind
+    s.close()
+
+
 @pytest.mark.parametrize("make", [_oh_nonhf_problem, _generic_problem], ids=["oh_nonhf_q10", "generic_q5"])
 @pytest.mark.parametrize("kind", [pytest.param(1, id="wave")] + BLOCK_KINDS)
 def test_collision_rules(make, kind):
