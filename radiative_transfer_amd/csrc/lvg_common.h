@@ -238,7 +238,32 @@ __device__ __forceinline__ double overlap_esc_func(const LvgDevProblem &P, const
 // ------------------------------------------------------------------------------
 // the layer's scalars into sm (one thread; SM: the block kernels' Smem / CollSmem or the
 // wave kernel's WaveLayer)
+// collision table tb's temperature interval at the layer's T (neutral) or Te (electrons)
 template <class SM>
+__device__ __forceinline__ void layer_table(const LvgDevProblem &P, int tb, double T, double Te, SM &sm) {
+    const double *tg = P.tab_tgrid + P.tab_tg_off[tb];
+    int jm = P.tab_jmax[tb];
+    double temp = (tb < P.nb_neutral) ? T : Te;
+    int lo = 0, hi = jm - 1;                  // collision_data::locate, strict '<'
+    while (hi - lo > 1) {
+        int j = lo + ((hi - lo) >> 1);
+        if (tg[j] < temp) lo = j; else hi = j;
+    }
+    sm.lo[tb] = lo;
+    double tmax = tg[jm - 1];
+    sm.teff[tb] = temp < tmax ? temp : tmax;
+    const int64_t imax = (int64_t)P.tab_nb_lev[tb] * (P.tab_nb_lev[tb] - 1) / 2;
+    sm.timax[tb] = imax;
+    sm.tcol[tb] = P.tab_coeff + P.tab_c_off[tb] + (int64_t)lo * imax;
+    sm.tder[tb] = P.tab_deriv + P.tab_c_off[tb] + (int64_t)lo * imax;
+    sm.tdt[tb] = tg[lo + 1] - tg[lo];
+    sm.tx[tb] = sm.teff[tb] - tg[lo];
+}
+
+// SPLIT: the table intervals through layer_table (the block kernels: same operations, a register
+// allocation with 116 fewer SGPR spills in solve_kernel at equal speed, profiles/r6/variants.txt
+// item 8's build); the wave kernel keeps the loop inline (its NM = 48 allocation spills more otherwise)
+template <class SM, bool SPLIT = false>
 __device__ __forceinline__ void layer_scalars(const LvgDevProblem &P, const LvgLaunch &Lc, int l, SM &sm) {
     const int64_t ld = Lc.soa_ld;
     const double *s = Lc.soa + Lc.lay_offset + l;
@@ -263,6 +288,10 @@ __device__ __forceinline__ void layer_scalars(const LvgDevProblem &P, const LvgL
             first = false;
         }
         sm.cc[k] = a;
+    }
+    if (SPLIT) {
+        for (int tb = 0; tb < P.nb_tables; tb++) layer_table(P, tb, T, Te, sm);
+        return;
     }
     for (int tb = 0; tb < P.nb_tables; tb++) {
         const double *tg = P.tab_tgrid + P.tab_tg_off[tb];

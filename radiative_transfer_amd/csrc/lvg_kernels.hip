@@ -168,7 +168,7 @@ __device__ __forceinline__ double block_max(double v, Smem &sm) {
 }
 
 __device__ __forceinline__ void layer_setup(const LvgDevProblem &P, const LvgLaunch &Lc, int l, Smem &sm) {
-    if (lvg_tid() == 0) layer_scalars(P, Lc, l, sm);
+    if (lvg_tid() == 0) layer_scalars<Smem, true>(P, Lc, l, sm);
     __syncthreads();
 }
 

@@ -8,8 +8,8 @@ product keeps the two changes that made it faster (opaque thread index, one call
 VGPRs spilled, 280 -> 100 B/lane, +3.4%) and drops the two that only removed spills
 (profiles/r5/variants.txt items 1-2). The later rank-16 rework (unconditional global L loads, item 14) runs
 +6% faster with more spills; round 6's pipelined collision build and typed fused chunk load
-(profiles/r6/variants.txt items 2 and 4: +1.8% and +0.7%, same box) end at 81 VGPRs / 278 SGPRs
-spilled, 152 B/lane (tools/kernel_notes.py at the final code). These tests pin that budget so that a change which pushes
+(profiles/r6/variants.txt items 2 and 4: +1.8% and +0.7%, same box) end at 81 VGPRs / 162 SGPRs
+spilled, 152 B/lane (tools/kernel_notes.py at the final code), inside round 5's budget. These tests pin that budget so that a change which pushes
 the LU back into heavy scratch use (round 4: 128 VGPRs, 564 SGPRs, 280 B/lane) fails here, on
 the CPU, before any GPU run; and they pin the LDS layout to two workgroups per CU.
 """
@@ -45,7 +45,7 @@ def test_block_solve_kernel_scratch_budget(notes, name):
     assert k["vgpr"] <= 256 and k["agpr"] == 0
     assert k["vgpr_spill"] <= 96, k
     assert k["scratch"] <= 192, k
-    assert k["sgpr_spill"] <= 320, k
+    assert k["sgpr_spill"] <= 256, k
 
 
 def test_block_kernel_lds_fits_two_workgroups_per_cu(notes):
