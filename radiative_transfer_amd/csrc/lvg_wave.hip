@@ -641,9 +641,8 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
     int lrow[NM];
 #pragma unroll
     for (int j = 0; j < NM; j++) {
-        const int jj = (j < N) ? j : 0;
-        krow[j] = K[row * ldk + jj];
-        lrow[j] = (j < N) ? li[row * ldk + jj] : -1;
+        krow[j] = K[row * ldk + j];          // +0 / -1 past N
+        lrow[j] = li[row * ldk + j];
     }
     if (!boundary) wave_start_pass(C, S, Lc, N, accel ? Lc.max_iter_acc : Lc.max_iter_plain, accel);
 #pragma unroll
@@ -690,7 +689,7 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
                         const int r = r0 + u;
                         kc[u] = K[r * ldk + d];
                         const int lv = li[r * ldk + d];
-                        lc[u] = (il && r < N) ? lv : -1;
+                        lc[u] = il ? lv : -1;
                     }
 #pragma unroll
                     for (int u = 0; u < 8; u++) yc[u] = sm.y[lc[u] >= 0 ? lc[u] : 0];
@@ -698,12 +697,9 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
                     // bit for bit, so the dependent chain is the subtractions alone
 #pragma unroll
                     for (int u = 0; u < 8; u++) {
-                        const int r = r0 + u;
-                        const bool on = r < N && r != d;
-                        const double t1 = on ? kc[u] : 0.;
-                        const double t2 = (on && lc[u] >= 0) ? yc[u] : 0.;
-                        dg = dg - t1;
-                        dg = dg - t2;
+                        // K[d][d] and the rows past N are +0, their line index -1
+                        dg = dg - kc[u];
+                        dg = dg - ((lc[u] >= 0) ? yc[u] : 0.);
                     }
                 }
                 if (!M.diag_interleaved) {
@@ -743,11 +739,11 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
                     v = (lc[u] >= 0) ? v + yc[u] : v;
                     v = (j == row) ? dg : v;
                     v = (row == 0) ? 1. : v;
-                    a[j] = (j < N) ? v : 0.;
-                    // columns past N subtract +0 (dg unchanged bit for bit): only the
-                    // subtractions are on the residual's dependent chain
-                    const double pv = v * pc[u];
-                    s = s - ((j < N) ? pv : 0.);
+                    // columns past N: K and the populations there are +0, so v * pc is +0 (the
+                    // subtraction leaves s unchanged bit for bit); a[j] past N is never read back
+                    // into a column below N (pivots, updates and the back substitution stop at N)
+                    a[j] = v;
+                    s = s - v * pc[u];
                 }
             }
             eq = wave_max(t < N ? fabs(s) : 0.);
@@ -835,10 +831,15 @@ solve_wave_kernel(const LvgDevProblem *__restrict__ Pp, const LvgLaunch *__restr
         else v = P.ov_g[e - o5];
         sh.grids[e] = v;
     }
-    for (int e = tid; e < N * N; e += blockDim.x) {
-        const int r = e / N, d = e - r * N;
-        li[r * ldk + d] = M.line_idx[e];
+    // the whole NM x ldk map: rows / columns past N hold -1 (no line), so the diagonal fold and the
+    // row assembly need no N masks; with K's diagonal and padding at +0 (below) and the populations
+    // past N at 0, every skipped term is a subtraction of +0
+    for (int e = tid; e < NM * ldk; e += blockDim.x) {
+        const int r = e / ldk, d = e - r * ldk;
+        li[e] = (r < N && d < N) ? M.line_idx[r * N + d] : -1;
     }
+    for (int e = lane_id(); e < NM * ldk; e += 64) K[e] = 0.;     // this wave's K: diagonal and padding stay +0
+    for (int e = lane_id(); e < WNMAX; e += 64) sh.w[w].pold[e] = 0.;
     __syncthreads();
     // the gamma / gamma-ratio grids non-decreasing (a NaN fails the test): the precondition of
     // the interval hints (ov_interval_hint)

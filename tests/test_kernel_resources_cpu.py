@@ -61,15 +61,14 @@ def test_debug_kernel_lu_without_spills(notes):
     assert k["vgpr_spill"] == 0 and k["scratch"] == 0, k
 
 
-@pytest.mark.parametrize("nm", [16, 24, 32, 40])
-def test_wave_kernel_small_nm_without_spills(notes, nm):
-    # OH-HF (N = 24) runs NM = 24; up to NM = 40 the wave kernel keeps everything in registers
+@pytest.mark.parametrize("nm", [16, 24, 32, 40, 48])
+def test_wave_kernel_without_scratch(notes, nm):
+    # OH-HF (N = 24) runs NM = 24, p-H2O (N = 45) NM = 48. Since round 6 the line-index map and K are
+    # padded in LDS (-1 / +0 past N and on K's diagonal), so the assembly needs no N or diagonal lane
+    # masks: up to NM = 48 nothing goes to scratch memory (NM = 48 had 55 VGPRs / 200 B/lane in round
+    # 5). A few VGPRs park in AGPRs at NM = 16, 32, 40, 48 (register copies, no memory).
     k = notes[f"void lvg::solve_wave_kernel<{nm}>"]
-    assert k["vgpr_spill"] == 0 and k["scratch"] == 0, k
-
-
-def test_wave_kernel_nm48_spill_budget(notes):
-    # p-H2O (N = 45) runs NM = 48: 55 VGPRs spilled (200 B/lane). The spill-free build (opaque lane
-    # index) measured 1-2% slower (profiles/r5/variants.txt item 9), so this pins the budget instead
-    k = notes["void lvg::solve_wave_kernel<48>"]
-    assert k["vgpr_spill"] <= 64 and k["scratch"] <= 256, k
+    assert k["scratch"] == 0, k
+    assert k["vgpr_spill"] <= 16, k
+    if nm == 24:
+        assert k["vgpr_spill"] == 0, k
