@@ -652,10 +652,11 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
         double eq = 0.;
         // N through an opaque SGPR copy each pass: otherwise the compiler hoists every
         // N-derived lane mask and K address of the unrolled loops out of the layer loop and
-        // spills them (v_writelane / v_readlane + s_nop on every use); measured: helps
-        // NM = 24, hurts NM = 48
+        // spills them (v_writelane / v_readlane + s_nop on every use). Round 5 measured it to help
+        // NM = 24 and hurt NM = 48; with the padded LDS map of round 6 it also helps NM = 48
+        // (SGPR spills 1058 -> 607, p-H2O -2%, profiles/r6/variants.txt item 14)
         int N = P.N;
-        if (NM <= 32) asm volatile("" : "+s"(N));
+        asm volatile("" : "+s"(N));
         if (boundary) {
             TSTAMP(tbd);
             wave_boundary_rows<NM>(S.A, N, a);
