@@ -41,7 +41,7 @@ constexpr int WNMAX = LVG_WAVE_NMAX;
 struct WaveLayer {                // per-wave LDS
     double pold[WNMAX], pnew[WNMAX], diag[WNMAX];
     int ivh[6][64];                     // grid interval hints, per lane (ov_interval_hint)
-    double y[WYCAP];
+    double y[WYCAP + 1];             // y[WYCAP] = +0: the line term of a pair with no line
     double hist_acc[32];
     double T, Te, vw, vgrad, nmol, ne;
     double cc[LVG_MAX_COMBOS];
@@ -657,6 +657,8 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
         // (SGPR spills 1058 -> 607, p-H2O -2%, profiles/r6/variants.txt item 14)
         int N = P.N;
         asm volatile("" : "+s"(N));
+        int rowo = row;                  // the lane's row, recomputed masks instead of hoisted spilled ones
+        asm volatile("" : "+v"(rowo));
         if (boundary) {
             TSTAMP(tbd);
             wave_boundary_rows<NM>(S.A, N, a);
@@ -693,14 +695,14 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
                         lc[u] = il ? lv : -1;
                     }
 #pragma unroll
-                    for (int u = 0; u < 8; u++) yc[u] = sm.y[lc[u] >= 0 ? lc[u] : 0];
+                    for (int u = 0; u < 8; u++) yc[u] = sm.y[lc[u] >= 0 ? lc[u] : WYCAP];
                     // the skipped terms become subtractions of +0, which leave dg unchanged
                     // bit for bit, so the dependent chain is the subtractions alone
 #pragma unroll
                     for (int u = 0; u < 8; u++) {
                         // K[d][d] and the rows past N are +0, their line index -1
                         dg = dg - kc[u];
-                        dg = dg - ((lc[u] >= 0) ? yc[u] : 0.);
+                        dg = dg - yc[u];                  // +0 where no line
                     }
                 }
                 if (!M.diag_interleaved) {
@@ -712,9 +714,9 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
 #pragma unroll
                         for (int u = 0; u < 8; u++) e[u] = (qb + u < q1) ? M.diag_ent[qb + u] : -1;
 #pragma unroll
-                        for (int u = 0; u < 8; u++) ye[u] = sm.y[e[u] >= 0 ? e[u] : 0];
+                        for (int u = 0; u < 8; u++) ye[u] = sm.y[e[u] >= 0 ? e[u] : WYCAP];
 #pragma unroll
-                        for (int u = 0; u < 8; u++) dg = dg - ((e[u] >= 0) ? ye[u] : 0.);
+                        for (int u = 0; u < 8; u++) dg = dg - ye[u];
                     }
                 }
             }
@@ -732,14 +734,14 @@ __device__ __forceinline__ bool wave_solve_layer(const LvgDevProblem &P, const L
                     pc[u] = sm.pold[j];        // j < NM <= WNMAX
                 }
 #pragma unroll
-                for (int u = 0; u < 8; u++) yc[u] = sm.y[lc[u] >= 0 ? lc[u] : 0];
+                for (int u = 0; u < 8; u++) yc[u] = sm.y[lc[u] >= 0 ? lc[u] : WYCAP];
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
                     const int j = j0 + u;
                     double v = kc[u];
-                    v = (lc[u] >= 0) ? v + yc[u] : v;
-                    v = (j == row) ? dg : v;
-                    v = (row == 0) ? 1. : v;
+                    v = v + yc[u];                        // K is never -0: K + (+0) == K
+                    v = (j == rowo) ? dg : v;
+                    v = (rowo == 0) ? 1. : v;
                     // columns past N: K and the populations there are +0, so v * pc is +0 (the
                     // subtraction leaves s unchanged bit for bit); a[j] past N is never read back
                     // into a column below N (pivots, updates and the back substitution stop at N)
@@ -841,6 +843,7 @@ solve_wave_kernel(const LvgDevProblem *__restrict__ Pp, const LvgLaunch *__restr
     }
     for (int e = lane_id(); e < NM * ldk; e += 64) K[e] = 0.;     // this wave's K: diagonal and padding stay +0
     for (int e = lane_id(); e < WNMAX; e += 64) sh.w[w].pold[e] = 0.;
+    if (lane_id() == 0) sh.w[w].y[WYCAP] = 0.;
     __syncthreads();
     // the gamma / gamma-ratio grids non-decreasing (a NaN fails the test): the precondition of
     // the interval hints (ov_interval_hint)

@@ -61,14 +61,13 @@ def test_debug_kernel_lu_without_spills(notes):
     assert k["vgpr_spill"] == 0 and k["scratch"] == 0, k
 
 
-@pytest.mark.parametrize("nm", [16, 24, 32, 40, 48])
-def test_wave_kernel_without_scratch(notes, nm):
-    # OH-HF (N = 24) runs NM = 24, p-H2O (N = 45) NM = 48. Since round 6 the line-index map and K are
-    # padded in LDS (-1 / +0 past N and on K's diagonal), so the assembly needs no N or diagonal lane
-    # masks: up to NM = 48 nothing goes to scratch memory (NM = 48 had 55 VGPRs / 200 B/lane in round
-    # 5). A few VGPRs park in AGPRs at NM = 16, 32, 40, 48 (register copies, no memory).
+@pytest.mark.parametrize("nm", [16, 24, 32, 40, 48, 56, 64])
+def test_wave_kernel_without_spills(notes, nm):
+    # OH-HF (N = 24) runs NM = 24, p-H2O (N = 45) NM = 48, the reference's OH-HF 56 NM = 56. Since
+    # round 6 the line-index map and K are padded in LDS (-1 / +0 past N and on K's diagonal), the
+    # line terms of pairs without a line read a +0 slot, and N and the lane's row reach the assembly
+    # through opaque per-pass copies, so no N / diagonal lane masks are hoisted and spilled: every
+    # instantiation keeps its VGPRs in registers and uses no scratch (round 5: NM = 48 spilled 55
+    # VGPRs, 200 B/lane; NM = 64 285 VGPRs, 880 B/lane; profiles/r6/variants.txt items 13, 14, 17).
     k = notes[f"void lvg::solve_wave_kernel<{nm}>"]
-    assert k["scratch"] == 0, k
-    assert k["vgpr_spill"] <= 16, k
-    if nm == 24:
-        assert k["vgpr_spill"] == 0, k
+    assert k["vgpr_spill"] == 0 and k["scratch"] == 0, k
